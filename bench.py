@@ -1,0 +1,224 @@
+"""Headline benchmark: OFDM symbols/s through the fused GPU modem path.
+
+Metric (BASELINE.json): OFDM symbols/sec at N_FFT=1024, 64-QAM.  Workload =
+BASELINE config (b): N_FFT=1024, 64-QAM, flat channel (flat_fading.npy, cp=0),
+no equaliser, AWGN at 24 dB (BER ~1e-4), complex64 arithmetic, Philox bits and
+noise generated on the device.  One step = one complete Simulation-run of the hot
+path over `--symbols` OFDM symbols per GPU (TX kernel, power all-reduce, RX
+kernel, counter all-reduce, results on the host).  Default 10 steps x 1e6
+symbols = the "1e7 symbols at one SNR" of config (b).
+
+Multi-GPU (torchrun): each rank simulates its contiguous share of the global
+symbol range of every step (weak scaling); exchanges: one all-reduce of the
+AWGN power statistics and one of the error counters per step (RCCL).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ofdm-based-systems_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+CONFIGS = {
+    # name: (N, M, channel, ratio, eq, snr_db, description)
+    "b": (1024, 64, "flat_fading", 1.0, "NONE", 24.0,
+          "config (b): N_FFT=1024, 64-QAM, flat channel (flat_fading.npy, cp=0), no equaliser, AWGN 24 dB"),
+    "c": (1024, 64, "severe_multipath", 1.0, "MMSE", 27.75,
+          "config (c): N_FFT=1024, 64-QAM, severe_multipath.npy (8 taps, cp=7), MMSE, AWGN 27.75 dB"),
+    "e": (4096, 256, "Lin-Phoong_P1", 1.0, "MMSE", 30.0,
+          "config (e): N_FFT=4096, 256-QAM, Lin-Phoong_P1.npy (4 taps, cp=3), MMSE, AWGN 30 dB"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def kernel_bytes_per_symbol(N: int, b: int, cp: int) -> int:
+    """Algorithmic bytes one OFDM symbol moves in ONE of the two kernels:
+    B_alg = 2*ceil(N*b/8) + 2*(N+cp)*8 per symbol is split evenly: each kernel touches the tx
+    bits once (map / comparator) and the complex64 channel stream once (write / read)."""
+    return math.ceil(N * b / 8) + (N + cp) * 8
+
+
+def _cpu_worker(args):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ofdm_oracle as O
+
+    seed, S, N, M, ch, cp, eq, snr = args
+    h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+    b = int(np.log2(M))
+    tx, nz = O.reference_streams(seed, S * N * b, S * (N + cp))
+    t0 = time.perf_counter()
+    O.run_fixed(tx, S * N * b, N, M, h, cp, eq, snr, nz)
+    return S, time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, per_worker: int):
+    """The NumPy oracle (a port of the reference path) on the host cores, bounded sample."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    N, M, ch, ratio, eq, snr, _ = cfg
+    h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+    cp = int(ratio * (len(h) - 1))
+    workers = max(1, min(16, os.cpu_count() or 1))
+    jobs = [(100 + i, per_worker, N, M, ch, cp, eq, snr) for i in range(workers)]
+    ctx = mp.get_context("spawn")
+    t0 = time.perf_counter()
+    with ctx.Pool(workers) as pool:
+        out = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    syms = sum(o[0] for o in out)
+    cpu_s = sum(o[1] for o in out)
+    return {
+        "value": syms / wall, "unit": "OFDM symbols/s", "cores": workers, "kind": "port",
+        "sample": f"{workers} processes x {per_worker} OFDM symbols of the same config through the NumPy "
+                  f"oracle (reference PCG64 bits + legacy-normal noise; stream generation untimed), "
+                  f"{cpu_s:.1f} s of CPU work, {wall:.1f} s wall incl. process start",
+        "per_core_symbols_per_s": syms / cpu_s,
+    }
+
+
+def pmc_traffic(config_name: str, symbols_per_launch: int):
+    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 --pmc summary
+    (profiles/pmc_summary.json, produced by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pm = json.load(f)
+    rec = pm.get(config_name)
+    if not rec:
+        return None
+    return {k: v * symbols_per_launch / rec["symbols_per_launch"] for k, v in rec["bytes_per_launch"].items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--symbols", type=int, default=1_000_000, help="OFDM symbols per GPU per step")
+    ap.add_argument("--config", default="b", choices=sorted(CONFIGS))
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--cpu-sample", type=int, default=1500, help="OFDM symbols per CPU worker")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+
+    from ofdm_based_systems import _backend as B
+    from ofdm_based_systems.constellation.models import QAMConstellationMapper
+    from ofdm_based_systems.engine import LinkEngine
+
+    cfg = CONFIGS[args.config]
+    N, M, ch, ratio, eq_name, snr, desc = cfg
+    h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+    cp = int(ratio * (len(h) - 1))
+    b = int(np.log2(M))
+    eq = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}[eq_name]
+    prec = B.OFDM_F32 if args.precision == "f32" else B.OFDM_F64
+    engine = LinkEngine(N, cp, h, eq, [QAMConstellationMapper(M).constellation], None, prec)
+    per_gpu = args.symbols
+    total = per_gpu * world
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    for i in range(args.warmup):
+        engine.run(total, snr, seed=10_000 + i, group=group)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    events = []
+    bit_errors = 0
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        st = engine.run(total, snr, seed=k, group=group, events=events)
+        bit_errors += st.bit_errors
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel average launch duration from HIP events on the launch stream
+    durs = {}
+    for name, n, e0, e1 in events:
+        durs.setdefault(name, []).append((e0.elapsed_time(e1) * 1e-3, n))
+    avg = {k: sum(d for d, _ in v) / len(v) for k, v in durs.items()}
+    dom = max(avg, key=avg.get)
+    sym_per_launch = durs[dom][0][1]
+    alg = kernel_bytes_per_symbol(N, b, cp) * sym_per_launch
+    achieved = alg / avg[dom] / 1e9
+    traffic = pmc_traffic(args.config, sym_per_launch)
+    value = total * args.steps / elapsed
+    out = {
+        "metric": "OFDM symbols/sec (1/2/4/8 GPU) at N_FFT=1024 64-QAM; BER ΔdB vs ref",
+        "value": value,
+        "unit": "OFDM symbols/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "c64 (f32)" if prec == B.OFDM_F32 else "c128 (f64)",
+        "data": "synthetic: Philox4x32-10 bits and Box-Muller AWGN generated on the GPU per (seed, symbol)",
+        "config": {
+            "workload": f"{desc}; {per_gpu} OFDM symbols per GPU per step",
+            "n_fft": N, "qam_order": M, "cp": cp, "channel": ch, "equalizer": eq_name, "snr_db": snr,
+            "symbols_per_step": total, "parallelism": f"symbol-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None if traffic is None else traffic.get(dom),
+            "alg_bytes_per_symbol": kernel_bytes_per_symbol(N, b, cp),
+            "symbols_per_launch": sym_per_launch,
+            "avg_launch_ms": {k: v * 1e3 for k, v in avg.items()},
+        },
+        "path_hbm_fraction": value * 2 * kernel_bytes_per_symbol(N, b, cp) / (HBM_PEAK_GBS * 1e9 * world),
+        "ber": bit_errors / (total * args.steps * N * b),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,625 @@
+// ofdm_kernels.hpp -- gfx950 kernels for the OFDM modem path (templated on the
+// real type R = float | double and on log2 N).  Instantiated per precision in
+// ofdm_kernels_f32.hip / ofdm_kernels_f64.hip, launched from ofdm_abi.hip.
+//
+// Hot path (Simulation.run, simulation/models.py:454-606) = two fused kernels:
+//   k_tx : bits -> LUT map -> IFFT(ortho) -> cyclic prefix -> L-tap FIR across symbol
+//          boundaries -> kept channel samples to HBM + sum|y|^2 / PAPR partials
+//   k_rx : HBM samples + AWGN -> FFT(ortho) -> ZF/MMSE -> slicer -> XOR/popcount
+//          against the tx bits -> u64 error counters
+// Everything between the two HBM touches of y lives in LDS/registers.
+#pragma once
+
+#include "ofdm_device.hpp"
+#include "ofdm_launch.hpp"
+
+namespace ofdm {
+
+// LDS carve helper: 16-byte aligned bump allocator over the dynamic LDS region.
+struct Carve {
+    unsigned char* p;
+    __device__ explicit Carve(unsigned char* base) : p(base) {}
+    template <typename T>
+    __device__ T* take(size_t n) {
+        T* r = reinterpret_cast<T*>(p);
+        p += (n * sizeof(T) + 15) & ~size_t(15);
+        return r;
+    }
+};
+
+extern __shared__ __attribute__((aligned(16))) unsigned char ofdm_smem[];
+
+// ============================================================ operator rows kernel
+// One workgroup iteration = SPB rows of N.  MODE: 0 = FFT (in place), 1 = modulate
+// (inverse FFT + cyclic prefix), 2 = demodulate (strip prefix, forward FFT, equalise).
+template <typename R, int LOGN, int MODE>
+__global__ __launch_bounds__(kBlock) void k_rows(RowsArgs a) {
+    using G = Geo<LOGN>;
+    using C = cpx<R>;
+    Carve cv(ofdm_smem);
+    C* tw = cv.take<C>(128);
+    C* data = cv.take<C>((size_t)G::SPB * G::PADN);
+    R* rowscale = cv.take<R>(G::SPB);
+    R* red = cv.take<R>(kBlock);
+    load_twiddles<R>(tw, (const C*)a.tw);
+    __syncthreads();
+
+    const C* in = (const C*)a.in;
+    C* out = (C*)a.out;
+    const bool inv = MODE == 1 || (MODE == 0 && a.inverse);
+    const int ls = threadIdx.x / G::TPS, t = threadIdx.x % G::TPS;
+    const R scale = (R)a.scale;
+    const int64_t ngroups = (a.n_rows + G::SPB - 1) / G::SPB;
+    for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+        const int64_t row0 = g * G::SPB;
+        // cooperative, coalesced load of SPB rows
+#pragma unroll
+        for (int j = 0; j < G::E; ++j) {
+            const int e = threadIdx.x + j * kBlock;
+            const int rl = e >> LOGN, k = e & (G::N - 1);
+            const int64_t row = row0 + rl;
+            C v = mk<R>(0, 0);
+            if (row < a.n_rows) {
+                const C* r = in + row * a.in_stride + a.in_off;
+                v = r[k];
+                if (MODE == 2 && k < a.zp) v = v + r[G::N + k];  // ZP overlap-add
+                v = cscale(v, scale);
+            }
+            data[rl * G::PADN + pad(k)] = v;
+        }
+        __syncthreads();
+        C* buf = data + ls * G::PADN;
+        if (inv)
+            fft_passes<R, LOGN, 0, true>(buf, tw, tw + 64, t);
+        else
+            fft_passes<R, LOGN, 0, false>(buf, tw, tw + 64, t);
+        if (MODE == 2 && a.eq == OFDM_EQ_MMSE) {
+            R p = 0;
+#pragma unroll
+            for (int i = 0; i < G::E; ++i) p += norm2(buf[pad(t + i * G::TPS)]);
+            p = group_sum<R, G::TPS>(p, red);
+            if (t == 0) {
+                const R sp = p / (R)G::N;
+                rowscale[ls] = a.gain_mean == 0.0 ? (R)INFINITY : (sp / (R)a.snr_lin) / (R)a.gain_mean;
+            }
+            __syncthreads();
+        }
+        const int olen = G::N + a.out_cp;
+        for (int e = threadIdx.x; e < G::SPB * olen; e += kBlock) {
+            const int rl = e / olen, m = e - rl * olen;
+            const int64_t row = row0 + rl;
+            if (row >= a.n_rows) continue;
+            C v;
+            if (MODE == 1 && a.zp) {
+                v = m < G::N ? data[rl * G::PADN + pad(m)] : mk<R>(0, 0);
+            } else {
+                const int k = m < a.out_cp ? G::N - a.out_cp + m : m - a.out_cp;
+                v = data[rl * G::PADN + pad(k)];
+            }
+            const int k = m < a.out_cp ? 0 : m - a.out_cp;  // subcarrier (MODE 2: out_cp = 0)
+            if (MODE == 2) {
+                if (a.eq == OFDM_EQ_ZF) {
+                    v = cmul(v, ((const C*)a.eq_a)[k]);
+                } else if (a.eq == OFDM_EQ_MMSE) {
+                    const C hc = ((const C*)a.eq_a)[k];
+                    const R d = ((const R*)a.eq_b)[k] + rowscale[rl];
+                    v = cmul(v, mk<R>(hc.re / d, hc.im / d));
+                }
+            }
+            out[row * a.out_stride + m] = v;
+        }
+        __syncthreads();
+    }
+}
+
+// ============================================================ equalise rows (no FFT)
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_equalize(EqArgs a) {
+    using C = cpx<R>;
+    __shared__ R red[kBlock / 64];
+    const C* Y = (const C*)a.Y;
+    C* Z = (C*)a.Z;
+    for (int64_t row = blockIdx.x; row < a.n_rows; row += gridDim.x) {
+        R nv = 0;
+        if (a.eq == OFDM_EQ_MMSE) {
+            R p = 0;
+            for (int k = threadIdx.x; k < a.n; k += kBlock) p += norm2(Y[row * a.n + k]);
+            p = block_sum<R>(p, red);
+            if (threadIdx.x == 0) red[0] = p;
+            __syncthreads();
+            p = red[0];
+            __syncthreads();
+            nv = a.gain_mean == 0.0 ? (R)INFINITY : ((p / (R)a.n) / (R)a.snr_lin) / (R)a.gain_mean;
+        }
+        for (int k = threadIdx.x; k < a.n; k += kBlock) {
+            C v = Y[row * a.n + k];
+            if (a.eq == OFDM_EQ_ZF) {
+                v = cmul(v, ((const C*)a.eq_a)[k]);
+            } else if (a.eq == OFDM_EQ_MMSE) {
+                const C hc = ((const C*)a.eq_a)[k];
+                const R d = ((const R*)a.eq_b)[k] + nv;
+                v = cmul(v, mk<R>(hc.re / d, hc.im / d));
+            }
+            Z[row * a.n + k] = v;
+        }
+    }
+}
+
+// ============================================================ constellation map (encode)
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_map(MapArgs a) {
+    using C = cpx<R>;
+    const C* lut = (const C*)a.lut;
+    C* out = (C*)a.out;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < a.n_out; e += stride) {
+        int64_t o;
+        int b, lutoff;
+        if (a.adaptive) {
+            const int64_t s = e / a.n_fft;
+            const int k = (int)(e - s * a.n_fft);
+            const ScInfo sc = a.sc[k];
+            if (sc.lut < 0) {
+                out[e] = mk<R>(0, 0);
+                continue;
+            }
+            o = s * a.bps + sc.bitoff;
+            b = sc.bits;
+            lutoff = a.axis[sc.lut].lut_off;
+        } else {
+            o = e * a.b;
+            b = a.b;
+            lutoff = 0;
+        }
+        // bits past the input read as zero (encode zero-pads, constellation/models.py:235-237)
+        uint32_t idx = 0;
+        for (int i = 0; i < b; ++i) {
+            const int64_t p = o + i;
+            const int64_t B = p >> 3;
+            const uint32_t bit = B < a.n_bytes ? (a.bytes[B] >> (7 - (int)(p & 7))) & 1u : 0u;
+            idx = (idx << 1) | bit;
+        }
+        out[e] = lut[lutoff + idx];
+    }
+}
+
+// ============================================================ brute-force NN (decode)
+// argmin_m |z - C_m| with np.abs semantics (hypot), first index on ties
+// (NNClassifier.classify, constellation/models.py:19-27).
+__device__ __forceinline__ int nn_index(double zr, double zi, const double* lut, int m) {
+    int best = 0;
+    double bd = hypot(zr - lut[0], zi - lut[1]);
+    for (int i = 1; i < m; ++i) {
+        const double d = hypot(zr - lut[2 * i], zi - lut[2 * i + 1]);
+        if (d < bd) {
+            bd = d;
+            best = i;
+        }
+    }
+    return best;
+}
+
+// decode: one thread per output byte; each element's NN index is recomputed by every
+// byte it touches.  Fixed mode: element e owns bits [e*b, e*b+b).  Adaptive mode:
+// element (s, k) owns bits [s*bps + off_k, +b_k) (constellation/adaptive.py:236-255).
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_demap(DemapArgs a) {
+    using C = cpx<R>;
+    const C* z = (const C*)a.z;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t B = (int64_t)blockIdx.x * kBlock + threadIdx.x; B < a.n_bytes; B += stride) {
+        uint32_t byte = 0;
+        const int64_t p0 = B * 8;
+        int64_t cur_e = -1;
+        uint32_t cur_idx = 0;
+        int cur_b = 0;
+        int64_t cur_o = 0;
+        for (int i = 0; i < 8; ++i) {
+            const int64_t p = p0 + i;
+            uint32_t bit = 0;
+            if (p < a.total_bits) {
+                int64_t e;
+                if (a.adaptive) {
+                    const int64_t s = p / a.bps;
+                    const int r = (int)(p - s * a.bps);
+                    // subcarrier holding stream bit r (binary search over bit offsets)
+                    int lo = 0, hi = a.n_active - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (a.sc[a.active[mid]].bitoff <= r) lo = mid; else hi = mid - 1;
+                    }
+                    e = s * a.n_fft + a.active[lo];
+                } else {
+                    e = p / a.b;
+                }
+                if (e != cur_e) {
+                    cur_e = e;
+                    int lutoff, m;
+                    if (a.adaptive) {
+                        const int k = (int)(e % a.n_fft);
+                        const ScInfo sc = a.sc[k];
+                        lutoff = a.axis[sc.lut].lut_off;
+                        m = 1 << sc.bits;
+                        cur_b = sc.bits;
+                        cur_o = (e / a.n_fft) * a.bps + sc.bitoff;
+                    } else {
+                        lutoff = 0;
+                        m = 1 << a.b;
+                        cur_b = a.b;
+                        cur_o = e * a.b;
+                    }
+                    const C v = z[e];
+                    cur_idx = (uint32_t)nn_index((double)v.re, (double)v.im, a.lut64 + 2 * lutoff, m);
+                }
+                const int pos = (int)(p - cur_o);
+                bit = (cur_idx >> (cur_b - 1 - pos)) & 1u;
+            }
+            byte = (byte << 1) | bit;
+        }
+        a.bytes[B] = (uint8_t)byte;
+    }
+}
+
+// ============================================================ channel convolution
+// y[n] = sum_l h[l] s[n-l] (s[<0] = 0), truncated to len (channel/models.py:52-55);
+// per-block sum |y|^2 into partials.
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_conv(ConvArgs a) {
+    using C = cpx<R>;
+    __shared__ double red[kBlock / 64];
+    const C* s = (const C*)a.s;
+    const C* h = (const C*)a.h;
+    C* y = (C*)a.y;
+    double acc = 0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t n = (int64_t)blockIdx.x * kBlock + threadIdx.x; n < a.len; n += stride) {
+        C v = mk<R>(0, 0);
+        for (int l = 0; l < a.L; ++l) {
+            if (n - l < 0) break;
+            v = v + cmul(h[l], s[n - l]);
+        }
+        y[n] = v;
+        acc += (double)norm2(v);
+    }
+    acc = block_sum<double>(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.x] = acc;
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_power(PowerArgs a) {
+    using C = cpx<R>;
+    __shared__ double red[kBlock / 64];
+    const C* y = (const C*)a.y;
+    double acc = 0;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t n = (int64_t)blockIdx.x * kBlock + threadIdx.x; n < a.len; n += stride)
+        acc += (double)norm2(y[n]);
+    acc = block_sum<double>(acc, red);
+    if (threadIdx.x == 0) a.partials[blockIdx.x] = acc;
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_awgn(AwgnArgs a) {
+    using C = cpx<R>;
+    C* y = (C*)a.y;
+    const double p = *a.power_sum / (double)a.len;
+    const double sigma = sqrt((p / a.snr_lin) / 2.0);
+    const R sg = (R)sigma;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t n = (int64_t)blockIdx.x * kBlock + threadIdx.x; n < a.len; n += stride) {
+        C v = y[n];
+        v.re += sg * (R)a.nr[n];
+        v.im += sg * (R)a.ni[n];
+        y[n] = v;
+    }
+}
+
+#ifdef OFDM_SUPPORT_KERNELS
+// Deterministic fixed-order reduction of per-block partials: stats[j] += / max= ...
+// field f is a max when bit f of max_mask is set, else a sum.
+__global__ __launch_bounds__(kBlock) void k_finalize(const double* partials, int nblocks, int nfields,
+                                                     int max_mask, double* stats) {
+    __shared__ double red[kBlock / 64];
+    for (int f = 0; f < nfields; ++f) {
+        const int op = (max_mask >> f) & 1;
+        double v = 0.0;
+        for (int i = threadIdx.x; i < nblocks; i += kBlock) {
+            const double x = partials[(int64_t)i * nfields + f];
+            v = op == 1 ? (x > v ? x : v) : v + x;
+        }
+        v = op == 1 ? block_max<double>(v, red) : block_sum<double>(v, red);
+        if (threadIdx.x == 0) stats[f] = op == 1 ? (v > stats[f] ? v : stats[f]) : stats[f] + v;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_nn_classify(const double* lut, int m, const double* z,
+                                                        int64_t n, int64_t* idx) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += stride)
+        idx[e] = nn_index(z[2 * e], z[2 * e + 1], lut, m);
+}
+
+#endif  // OFDM_SUPPORT_KERNELS
+
+// ============================================================ fused TX
+// Each symbol group (TPS threads) walks `chunk` consecutive OFDM symbols so the FIR
+// tail (last L-1 samples of the previous symbol) is carried in LDS; the first symbol
+// of a chunk regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
+template <typename R>
+__device__ __forceinline__ void stage_bits(const TxRxCommon& a, int64_t s_global, uint8_t* lb,
+                                           int nbytes_lds, int t, int tps, int& base_bit) {
+    if (a.bits) {
+        const int64_t bit0 = s_global * a.bps;
+        const int64_t B0 = bit0 >> 3;
+        base_bit = (int)(bit0 & 7);
+        const int64_t total_bytes = a.n_bytes;
+        for (int i = t; i < nbytes_lds; i += tps) {
+            const int64_t B = B0 + i;
+            lb[i] = (s_global >= 0 && B < total_bytes) ? a.bits[B] : (uint8_t)0;
+        }
+    } else {
+        base_bit = 0;
+        const int nblk = (a.bps + 127) >> 7;
+        for (int blk = t; blk < nblk; blk += tps) {
+            const u4 o = philox_bits_block(a.seed, s_global, (uint32_t)blk);
+            const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int B = (blk * 4 + q) * 4;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (B + i < nbytes_lds) lb[B + i] = (uint8_t)(w[q] >> (24 - 8 * i));
+            }
+        }
+    }
+}
+
+template <typename R, int LOGN>
+__global__ __launch_bounds__(kBlock) void k_tx(TxArgs a) {
+    using G = Geo<LOGN>;
+    using C = cpx<R>;
+    const TxRxCommon& cm = a.c;
+    Carve cv(ofdm_smem);
+    C* tw = cv.take<C>(128);
+    C* lut = cv.take<C>(cm.lut_len);
+    C* h = cv.take<C>(32);
+    AxisInfo* axis = cv.take<AxisInfo>(4);
+    C* data = cv.take<C>((size_t)G::SPB * G::PADN);
+    C* tail = cv.take<C>((size_t)G::SPB * 32);
+    const int nbl = cm.bytes_per_sym_lds;
+    uint8_t* bitsl = cv.take<uint8_t>((size_t)G::SPB * nbl);
+    double* red = cv.take<double>(kBlock / 64);
+
+    load_twiddles<R>(tw, (const C*)cm.tw);
+    for (int i = threadIdx.x; i < cm.lut_len; i += kBlock) lut[i] = ((const C*)cm.lut)[i];
+    if (threadIdx.x < a.L) h[threadIdx.x] = ((const C*)a.h)[threadIdx.x];
+    if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
+    __syncthreads();
+
+    const int ls = threadIdx.x / G::TPS, t = threadIdx.x % G::TPS;
+    C* buf = data + ls * G::PADN;
+    C* tl = tail + ls * 32;
+    uint8_t* lb = bitsl + ls * nbl;
+    C* yout = (C*)a.y;
+    const int cp = cm.cp, L = a.L;
+    const R scale = (R)cm.scale;
+    const int64_t ngroups = (cm.n_sym + a.chunk - 1) / a.chunk;
+    const int64_t niter = (ngroups + G::SPB - 1) / G::SPB;
+    double py = 0, px = 0, mx = 0;
+
+    for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
+        const int64_t grp = it * G::SPB + ls;
+        const int64_t sbeg = grp * a.chunk;  // local symbol index
+        for (int c = (L > 1 ? -1 : 0); c < a.chunk; ++c) {
+            const int64_t sl = sbeg + c;
+            const int64_t sg = cm.sym0 + sl;
+            const bool active = grp < ngroups && sl < cm.n_sym && sg >= 0;
+            int base_bit = 0;
+            if (active) stage_bits<R>(cm, sg, lb, nbl, t, G::TPS, base_bit);
+            __syncthreads();
+            // map (QAMConstellationMapper.encode, constellation/models.py:240-246) with the
+            // ortho 1/sqrt(N) of ifft(norm="ortho") folded in
+#pragma unroll
+            for (int i = 0; i < G::E; ++i) {
+                const int k = t + i * G::TPS;
+                C v = mk<R>(0, 0);
+                if (active) {
+                    if (cm.adaptive) {
+                        const ScInfo sc = cm.sc[k];
+                        if (sc.lut >= 0) {
+                            const uint32_t idx = extract_bits(lb, base_bit + sc.bitoff, sc.bits);
+                            v = lut[axis[sc.lut].lut_off + idx];
+                        }
+                    } else {
+                        v = lut[extract_bits(lb, base_bit + (int64_t)k * cm.b, cm.b)];
+                    }
+                }
+                buf[pad(k)] = cscale(v, scale);
+            }
+            __syncthreads();
+            fft_passes<R, LOGN, 0, true>(buf, tw, tw + 64, t);
+            // x = buf (natural order).  Serial stream of this symbol: ext(m) for
+            // m in [0, N+cp): m < cp -> x[N-cp+m], else x[m-cp]; ext(<0) = previous tail.
+            if (active && c >= 0) {
+                for (int m = t; m < G::N + cp; m += G::TPS) {
+                    C yv = mk<R>(0, 0);
+                    for (int l = 0; l < L; ++l) {
+                        const int q = m - l;
+                        C xv;
+                        if (q < 0)
+                            xv = tl[L - 1 + q];
+                        else
+                            xv = buf[pad(q < cp ? G::N - cp + q : q - cp)];
+                        yv = yv + cmul(h[l], xv);
+                    }
+                    py += (double)norm2(yv);
+                    const C xm = buf[pad(m < cp ? G::N - cp + m : m - cp)];
+                    const double p2 = (double)norm2(xm);
+                    px += p2;
+                    mx = p2 > mx ? p2 : mx;
+                    if (yout && m >= cp) yout[sl * G::N + (m - cp)] = yv;
+                }
+            }
+            __syncthreads();
+            if (L > 1 && t < L - 1) {
+                // tail for the next symbol: last L-1 samples of this symbol's stream
+                // (host guarantees L-1 <= N); the stream starts with zeros (sg < 0)
+                const int m = G::N + cp - (L - 1) + t;
+                tl[t] = active ? buf[pad(m < cp ? G::N - cp + m : m - cp)] : mk<R>(0, 0);
+            }
+            __syncthreads();
+        }
+    }
+    py = block_sum<double>(py, red);
+    px = block_sum<double>(px, red);
+    mx = block_max<double>(mx, red);
+    if (threadIdx.x == 0) {
+        a.partials[blockIdx.x * 3 + 0] = py;
+        a.partials[blockIdx.x * 3 + 1] = px;
+        a.partials[blockIdx.x * 3 + 2] = mx;
+    }
+}
+
+// ============================================================ fused RX
+template <typename R, int LOGN>
+__global__ __launch_bounds__(kBlock) void k_rx(RxArgs a) {
+    using G = Geo<LOGN>;
+    using C = cpx<R>;
+    const TxRxCommon& cm = a.c;
+    Carve cv(ofdm_smem);
+    C* tw = cv.take<C>(128);
+    AxisInfo* axis = cv.take<AxisInfo>(4);
+    C* data = cv.take<C>((size_t)G::SPB * G::PADN);
+    const int nbl = cm.bytes_per_sym_lds;
+    uint8_t* bitsl = cv.take<uint8_t>((size_t)G::SPB * nbl);
+    R* red = cv.take<R>(kBlock);
+    double* redd = cv.take<double>(kBlock / 64);
+
+    load_twiddles<R>(tw, (const C*)cm.tw);
+    if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
+    __syncthreads();
+
+    const int ls = threadIdx.x / G::TPS, t = threadIdx.x % G::TPS;
+    C* buf = data + ls * G::PADN;
+    uint8_t* lb = bitsl + ls * nbl;
+    const C* yin = (const C*)a.y;
+    const int cp = cm.cp;
+    const R scale = (R)cm.scale;
+
+    // sigma from the whole-stream mean power (noise/models.py:13-22)
+    R sigma = 0;
+    if (a.noise_on) {
+        const double p = a.stats[0] / (double)a.total_samples;
+        sigma = (R)sqrt((p / a.snr_lin) / 2.0);
+    }
+    const int64_t niter = (cm.n_sym + G::SPB - 1) / G::SPB;
+    uint64_t be = 0, se = 0;
+
+    for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
+        const int64_t sl = it * G::SPB + ls;
+        const int64_t sg = cm.sym0 + sl;
+        const bool active = sl < cm.n_sym;
+        int base_bit = 0;
+        if (active) stage_bits<R>(cm, sg, lb, nbl, t, G::TPS, base_bit);
+        // load kept samples + AWGN, ortho scale folded in
+        if (a.nr) {
+#pragma unroll
+            for (int i = 0; i < G::E; ++i) {
+                const int k = t + i * G::TPS;
+                C v = mk<R>(0, 0);
+                if (active) {
+                    v = yin[sl * G::N + k];
+                    if (a.noise_on) {
+                        const int64_t gi = sg * (G::N + cp) + cp + k;
+                        v.re += sigma * (R)a.nr[gi];
+                        v.im += sigma * (R)a.ni[gi];
+                    }
+                }
+                buf[pad(k)] = cscale(v, scale);
+            }
+        } else {
+            // Philox noise: thread owns sample pairs (2p, 2p+1)
+#pragma unroll
+            for (int i = 0; i < (G::E + 1) / 2; ++i) {
+                const int p = t + i * G::TPS;
+                if (2 * p >= G::N) break;
+                C v0 = mk<R>(0, 0), v1 = mk<R>(0, 0);
+                if (active) {
+                    v0 = yin[sl * G::N + 2 * p];
+                    if (2 * p + 1 < G::N) v1 = yin[sl * G::N + 2 * p + 1];
+                    if (a.noise_on) {
+                        float r0, i0, r1, i1;
+                        philox_noise_pair(cm.seed, sg, (uint32_t)p, r0, i0, r1, i1);
+                        v0.re += sigma * (R)r0;
+                        v0.im += sigma * (R)i0;
+                        v1.re += sigma * (R)r1;
+                        v1.im += sigma * (R)i1;
+                    }
+                }
+                buf[pad(2 * p)] = cscale(v0, scale);
+                if (2 * p + 1 < G::N) buf[pad(2 * p + 1)] = cscale(v1, scale);
+            }
+        }
+        __syncthreads();
+        fft_passes<R, LOGN, 0, false>(buf, tw, tw + 64, t);
+        // MMSE noise variance per OFDM symbol (equalization/models.py:39-49)
+        R nv = 0;
+        if (cm.eq == OFDM_EQ_MMSE) {
+            R p = 0;
+#pragma unroll
+            for (int i = 0; i < G::E; ++i) p += norm2(buf[pad(t + i * G::TPS)]);
+            p = group_sum<R, G::TPS>(p, red);
+            nv = cm.gain_mean == 0.0 ? (R)INFINITY : ((p / (R)G::N) / (R)a.snr_lin) / (R)cm.gain_mean;
+        }
+        if (active) {
+            const int64_t sbit = sg * cm.bps;
+            const bool all_valid = sbit + cm.bps <= a.n_valid_bits;
+#pragma unroll
+            for (int i = 0; i < G::E; ++i) {
+                const int k = t + i * G::TPS;
+                C v = buf[pad(k)];
+                if (cm.eq == OFDM_EQ_ZF) {
+                    v = cmul(v, ((const C*)cm.eq_a)[k]);
+                } else if (cm.eq == OFDM_EQ_MMSE) {
+                    const C hc = ((const C*)cm.eq_a)[k];
+                    const R d = ((const R*)cm.eq_b)[k] + nv;
+                    v = cmul(v, mk<R>(hc.re / d, hc.im / d));
+                }
+                if (sl < a.z_keep) ((C*)a.z_out)[sl * G::N + k] = v;
+                int b, off, ai;
+                if (cm.adaptive) {
+                    const ScInfo sc = cm.sc[k];
+                    if (sc.lut < 0) continue;
+                    b = sc.bits;
+                    off = sc.bitoff;
+                    ai = sc.lut;
+                } else {
+                    b = cm.b;
+                    off = k * cm.b;
+                    ai = 0;
+                }
+                const uint32_t ridx = slice<R>(v, axis[ai]);
+                const uint32_t tidx = extract_bits(lb, base_bit + off, b);
+                uint32_t d = ridx ^ tidx;
+                se += d != 0u;
+                if (!all_valid) {
+                    const int64_t nv_bits = a.n_valid_bits - (sbit + off);
+                    const int keep = nv_bits <= 0 ? 0 : (nv_bits >= b ? b : (int)nv_bits);
+                    d &= ((1u << keep) - 1u) << (b - keep);
+                }
+                be += __popc(d);
+            }
+        }
+        __syncthreads();
+    }
+    unsigned long long fb = be, fs = se;
+    fb = block_sum<unsigned long long>(fb, (unsigned long long*)redd);
+    fs = block_sum<unsigned long long>(fs, (unsigned long long*)redd);
+    if (threadIdx.x == 0) {
+        if (fb) atomicAdd((unsigned long long*)&a.counters[0], fb);
+        if (fs) atomicAdd((unsigned long long*)&a.counters[1], fs);
+    }
+}
+
+}  // namespace ofdm

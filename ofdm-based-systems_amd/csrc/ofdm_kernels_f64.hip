@@ -1,0 +1,22 @@
+// complex128 (parity mode / operator API) instantiation of every kernel launcher,
+// plus the precision-independent support kernels.
+#define OFDM_SUPPORT_KERNELS 1
+#include "ofdm_kernels_inst.hpp"
+
+namespace ofdm {
+OFDM_INSTANTIATE(double)
+
+hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int max_mask,
+                           double* stats, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, s, partials, nblocks, nfields, max_mask, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_nn_classify(const double* lut, int m, const double* z, int64_t n, int64_t* idx,
+                              hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_nn_classify, dim3(clamp_grid((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
+                       lut, m, z, n, idx);
+    return hipGetLastError();
+}
+}  // namespace ofdm

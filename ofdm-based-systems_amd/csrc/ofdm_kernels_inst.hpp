@@ -1,0 +1,150 @@
+// ofdm_kernels_inst.hpp -- launcher definitions; included once per precision by
+// ofdm_kernels_f32.hip / ofdm_kernels_f64.hip (explicit instantiation at the end of
+// each), so the two precisions compile in parallel.
+#pragma once
+
+#include <algorithm>
+
+#include "ofdm_kernels.hpp"
+
+namespace ofdm {
+
+#define OFDM_LOGN_CASES(X) \
+    X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+
+template <typename F>
+static hipError_t set_smem(F fn, size_t bytes) {
+    // Dynamic LDS above 64 KiB must be opted in per kernel; idempotent and cheap.
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+static inline int clamp_grid(int64_t want) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(want, kMaxGrid));
+}
+
+template <typename R, int LOGN, int MODE>
+static hipError_t rows_one(const RowsArgs& a, hipStream_t s) {
+    const size_t sm = smem_rows<R>(LOGN);
+    auto fn = k_rows<R, LOGN, MODE>;
+    static const hipError_t attr = set_smem(fn, sm);
+    if (attr != hipSuccess) return attr;
+    const int64_t groups = (a.n_rows + Geo<LOGN>::SPB - 1) / Geo<LOGN>::SPB;
+    hipLaunchKernelGGL(fn, dim3(clamp_grid(groups)), dim3(kBlock), sm, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_rows(int logn, int mode, const RowsArgs& a, hipStream_t s) {
+    if (a.n_rows <= 0) return hipSuccess;
+#define OFDM_ROWS_CASE(L)                                   \
+    case L:                                                 \
+        if (mode == 0) return rows_one<R, L, 0>(a, s);      \
+        if (mode == 1) return rows_one<R, L, 1>(a, s);      \
+        return rows_one<R, L, 2>(a, s);
+    switch (logn) {
+        OFDM_LOGN_CASES(OFDM_ROWS_CASE)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef OFDM_ROWS_CASE
+}
+
+template <typename R>
+hipError_t launch_equalize(const EqArgs& a, hipStream_t s) {
+    if (a.n_rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_equalize<R>, dim3(clamp_grid(a.n_rows)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_map(const MapArgs& a, hipStream_t s) {
+    if (a.n_out <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_map<R>, dim3(clamp_grid((a.n_out + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_demap(const DemapArgs& a, hipStream_t s) {
+    if (a.n_bytes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_demap<R>, dim3(clamp_grid((a.n_bytes + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_conv(const ConvArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_conv<R>, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_power(const PowerArgs& a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(k_power<R>, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
+    if (a.len <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_awgn<R>, dim3(clamp_grid((a.len + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename R, int LOGN>
+static hipError_t tx_one(const TxArgs& a, int grid, hipStream_t s) {
+    const size_t sm = smem_tx<R>(LOGN, a.c.lut_len, a.c.bytes_per_sym_lds);
+    auto fn = k_tx<R, LOGN>;
+    hipError_t e = set_smem(fn, sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), sm, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_tx(int logn, const TxArgs& a, int grid, hipStream_t s) {
+#define OFDM_TX_CASE(L) \
+    case L:             \
+        return tx_one<R, L>(a, grid, s);
+    switch (logn) {
+        OFDM_LOGN_CASES(OFDM_TX_CASE)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef OFDM_TX_CASE
+}
+
+template <typename R, int LOGN>
+static hipError_t rx_one(const RxArgs& a, int grid, hipStream_t s) {
+    const size_t sm = smem_rx<R>(LOGN, a.c.bytes_per_sym_lds);
+    auto fn = k_rx<R, LOGN>;
+    hipError_t e = set_smem(fn, sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), sm, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
+hipError_t launch_rx(int logn, const RxArgs& a, int grid, hipStream_t s) {
+#define OFDM_RX_CASE(L) \
+    case L:             \
+        return rx_one<R, L>(a, grid, s);
+    switch (logn) {
+        OFDM_LOGN_CASES(OFDM_RX_CASE)
+        default:
+            return hipErrorInvalidValue;
+    }
+#undef OFDM_RX_CASE
+}
+
+#define OFDM_INSTANTIATE(R)                                                         \
+    template hipError_t launch_rows<R>(int, int, const RowsArgs&, hipStream_t);     \
+    template hipError_t launch_equalize<R>(const EqArgs&, hipStream_t);             \
+    template hipError_t launch_map<R>(const MapArgs&, hipStream_t);                 \
+    template hipError_t launch_demap<R>(const DemapArgs&, hipStream_t);             \
+    template hipError_t launch_conv<R>(const ConvArgs&, int, hipStream_t);          \
+    template hipError_t launch_power<R>(const PowerArgs&, int, hipStream_t);        \
+    template hipError_t launch_awgn<R>(const AwgnArgs&, hipStream_t);               \
+    template hipError_t launch_tx<R>(int, const TxArgs&, int, hipStream_t);         \
+    template hipError_t launch_rx<R>(int, const RxArgs&, int, hipStream_t);
+
+}  // namespace ofdm

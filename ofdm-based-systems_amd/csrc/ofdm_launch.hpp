@@ -1,0 +1,182 @@
+// ofdm_launch.hpp -- POD kernel argument blocks shared by host (ofdm_abi.hip) and
+// device (ofdm_kernels.hpp), plus the per-precision launcher entry points.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ofdm_device.hpp"
+#include "ofdm_hip.h"
+
+namespace ofdm {
+
+constexpr int kMaxGrid = 4096;  // partial-sum workspace rows
+constexpr int kMaxTaps = 32;
+constexpr int kMaxLut = 512;
+
+struct RowsArgs {
+    const void* in;
+    void* out;
+    int64_t n_rows, in_stride, out_stride;
+    int in_off, out_cp, inverse, eq;
+    int zp;  // zero-padding length: modulate appends zeros, demodulate folds the tail (overlap-add)
+    double scale, snr_lin, gain_mean;
+    const void* tw;
+    const void* eq_a;
+    const void* eq_b;
+};
+
+struct EqArgs {
+    const void* Y;
+    void* Z;
+    int64_t n_rows;
+    int n, eq;
+    double snr_lin, gain_mean;
+    const void* eq_a;
+    const void* eq_b;
+};
+
+struct MapArgs {
+    const uint8_t* bytes;
+    int64_t n_bytes, n_out;
+    void* out;
+    const void* lut;
+    int b, adaptive, n_fft, bps;
+    const ScInfo* sc;
+    const AxisInfo* axis;
+};
+
+struct DemapArgs {
+    const void* z;
+    uint8_t* bytes;
+    int64_t n_bytes, total_bits;
+    int b, adaptive, n_fft, bps, n_active;
+    const ScInfo* sc;
+    const AxisInfo* axis;
+    const int32_t* active;
+    const double* lut64;
+};
+
+struct ConvArgs {
+    const void* s;
+    void* y;
+    int64_t len;
+    const void* h;
+    int L;
+    double* partials;
+};
+
+struct PowerArgs {
+    const void* y;
+    int64_t len;
+    double* partials;
+};
+
+struct AwgnArgs {
+    void* y;
+    int64_t len;
+    const double* nr;
+    const double* ni;
+    const double* power_sum;
+    double snr_lin;
+};
+
+struct TxRxCommon {
+    const uint8_t* bits;
+    int64_t n_bytes;
+    uint64_t seed;
+    int64_t sym0, n_sym;
+    const void* tw;
+    const void* lut;
+    int lut_len;
+    const AxisInfo* axis;
+    int n_axis;
+    const ScInfo* sc;
+    int adaptive, b, bps, cp, eq;
+    int bytes_per_sym_lds;
+    double scale, gain_mean;
+    const void* eq_a;
+    const void* eq_b;
+};
+
+struct TxArgs {
+    TxRxCommon c;
+    void* y;
+    double* partials;
+    const void* h;
+    int L;
+    int chunk;
+};
+
+struct RxArgs {
+    TxRxCommon c;
+    const void* y;
+    const double* nr;
+    const double* ni;
+    const double* stats;
+    int64_t total_samples;
+    double snr_lin;
+    int noise_on;
+    int64_t n_valid_bits;
+    uint64_t* counters;
+    void* z_out;
+    int64_t z_keep;
+};
+
+// ---- LDS footprints (must mirror the Carve sequences in ofdm_kernels.hpp)
+inline size_t rnd16(size_t n) { return (n + 15) & ~size_t(15); }
+inline int geo_spb(int logn) {
+    const int loge = logn < 4 ? logn : 4;
+    return 256 / ((1 << logn) >> loge);
+}
+inline int geo_padn(int logn) { return (1 << logn) + ((1 << logn) >> 4) + 1; }
+
+template <typename R>
+inline size_t smem_rows(int logn) {
+    const size_t c = 2 * sizeof(R);
+    const int spb = geo_spb(logn);
+    return rnd16(128 * c) + rnd16((size_t)spb * geo_padn(logn) * c) + rnd16(spb * sizeof(R)) +
+           rnd16(256 * sizeof(R));
+}
+template <typename R>
+inline size_t smem_tx(int logn, int lut_len, int nbl) {
+    const size_t c = 2 * sizeof(R);
+    const int spb = geo_spb(logn);
+    return rnd16(128 * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(4 * sizeof(AxisInfo)) +
+           rnd16((size_t)spb * geo_padn(logn) * c) + rnd16((size_t)spb * 32 * c) +
+           rnd16((size_t)spb * nbl) + rnd16(4 * sizeof(double));
+}
+template <typename R>
+inline size_t smem_rx(int logn, int nbl) {
+    const size_t c = 2 * sizeof(R);
+    const int spb = geo_spb(logn);
+    return rnd16(128 * c) + rnd16(4 * sizeof(AxisInfo)) + rnd16((size_t)spb * geo_padn(logn) * c) +
+           rnd16((size_t)spb * nbl) + rnd16(256 * sizeof(R)) + rnd16(4 * sizeof(double));
+}
+
+// ---- launchers (instantiated for float and double in ofdm_kernels_f{32,64}.hip)
+template <typename R>
+hipError_t launch_rows(int logn, int mode, const RowsArgs& a, hipStream_t s);
+template <typename R>
+hipError_t launch_equalize(const EqArgs& a, hipStream_t s);
+template <typename R>
+hipError_t launch_map(const MapArgs& a, hipStream_t s);
+template <typename R>
+hipError_t launch_demap(const DemapArgs& a, hipStream_t s);
+template <typename R>
+hipError_t launch_conv(const ConvArgs& a, int grid, hipStream_t s);
+template <typename R>
+hipError_t launch_power(const PowerArgs& a, int grid, hipStream_t s);
+template <typename R>
+hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s);
+template <typename R>
+hipError_t launch_tx(int logn, const TxArgs& a, int grid, hipStream_t s);
+template <typename R>
+hipError_t launch_rx(int logn, const RxArgs& a, int grid, hipStream_t s);
+
+hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int max_mask,
+                           double* stats, hipStream_t s);
+hipError_t launch_nn_classify(const double* lut, int m, const double* z, int64_t n, int64_t* idx,
+                              hipStream_t s);
+
+}  // namespace ofdm

@@ -1,0 +1,189 @@
+"""Fused GPU link engine: the hot path of ``Simulation.run`` (simulation/models.py:454-606).
+
+One :class:`LinkEngine` = one modem configuration (N, prefix, channel, LUTs,
+equaliser) held in a libofdm_hip plan.  :meth:`LinkEngine.run` pushes S OFDM
+symbols through
+
+    ofdm_tx  : bits -> map -> IFFT(ortho) + CP -> FIR (across symbol boundaries)
+               -> kept channel samples y (HBM) + sum|y|^2 / PAPR statistics
+    [all-reduce of the statistics across ranks]
+    ofdm_rx  : y + AWGN (sigma from the global mean power) -> FFT(ortho) -> ZF/MMSE
+               -> slicer -> XOR/popcount against the tx bits -> u64 counters
+    [all-reduce of the counters across ranks]
+
+Bit / noise sources:
+  * reference mode -- the caller passes the reference's packed PCG64 bytes and its
+    legacy-RNG normals (the whole serial stream): integer counts are bit-exact with
+    the reference;
+  * philox mode    -- bits and noise are generated inside the kernels from a
+    counter-based Philox4x32-10 keyed by (seed, global symbol), so nothing but y
+    touches HBM and results do not depend on the number of GPUs.
+
+Multi-GPU: symbols [r*S/R, (r+1)*S/R) go to rank r; the only exchanges are one
+all-reduce of three doubles (the AWGN power is a whole-stream mean,
+noise/models.py:14) and one of the two u64 counters.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from ofdm_based_systems import _backend as B
+
+DEFAULT_Y_BUDGET = 64 << 30  # bytes of kept channel samples held at once per GPU
+
+
+@dataclass
+class LinkStats:
+    bit_errors: int
+    symbol_errors: int
+    num_ofdm_symbols: int
+    power_sum: float      # sum |y|^2 over the whole serial stream (all ranks)
+    x_power_sum: float    # sum |x|^2 over the modulated stream incl. prefix
+    x_peak: float         # max |x|^2
+    samples: int          # S * (N + cp)
+    papr_db: float
+    received: Optional[np.ndarray] = None
+    timings: dict = field(default_factory=dict)
+
+
+def shard(n: int, rank: int, world: int) -> tuple:
+    """Contiguous [lo, hi) share of n items for one rank."""
+    lo = (n * rank) // world
+    hi = (n * (rank + 1)) // world
+    return lo, hi
+
+
+class LinkEngine:
+    def __init__(self, n_fft: int, cp: int, h_raw: np.ndarray, equalizer: int, luts: Sequence[np.ndarray],
+                 sc_lut: Optional[np.ndarray] = None, precision: int = B.OFDM_F64):
+        self.plan = B.Plan(n_fft=n_fft, cp=cp, precision=precision, equalizer=equalizer, luts=list(luts),
+                           sc_lut=sc_lut, h_raw=np.asarray(h_raw, np.complex128))
+        self.n_fft = n_fft
+        self.cp = cp
+        self.bps = self.plan.bits_per_ofdm_symbol
+        self.adaptive = self.plan.adaptive
+        self.cdtype = self.plan.cdtype
+        self._lib = B.lib()
+
+    # ------------------------------------------------------------------ helpers
+    def valid_bits(self, n_sym: int) -> int:
+        """Bits the reference compares: all of them in FIXED mode, whole bytes in adaptive mode
+        (AdaptiveConstellationMapper.decode drops a partial byte, constellation/adaptive.py:259-263)."""
+        total = n_sym * self.bps
+        return (total // 8) * 8 if self.adaptive else total
+
+    @staticmethod
+    def _timed(events, name, n_sym, fn):
+        if events is None:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        events.append((name, n_sym, e0, e1))
+
+    def tx(self, stream, bits_d, seed, sym0, n_sym, y, stats):
+        B.check(self._lib.ofdm_tx(self.plan.handle, stream, B.ptr(bits_d), int(seed), int(sym0), int(n_sym),
+                                  B.ptr(y), B.ptr(stats)))
+
+    def rx(self, stream, y, nr, ni, seed, stats, total_samples, snr_db, noise_on, bits_d, sym0, n_sym,
+           n_valid, counters, z_out=None, z_keep=0):
+        B.check(self._lib.ofdm_rx(self.plan.handle, stream, B.ptr(y), B.ptr(nr), B.ptr(ni), int(seed),
+                                  B.ptr(stats), int(total_samples), float(snr_db), int(noise_on), B.ptr(bits_d),
+                                  int(sym0), int(n_sym), int(n_valid), B.ptr(counters), B.ptr(z_out),
+                                  int(z_keep)))
+
+    # ------------------------------------------------------------------ run
+    def run(self, n_sym: int, snr_db: float, *, bits: Optional[np.ndarray] = None,
+            normals: Optional[tuple] = None, seed: int = 0, noise_on: bool = True, keep_symbols: int = 0,
+            group=None, y_budget: int = DEFAULT_Y_BUDGET, batch: Optional[int] = None,
+            n_valid_bits: Optional[int] = None, events: Optional[list] = None) -> LinkStats:
+        """Simulate global OFDM symbols [0, n_sym) (this rank's shard when ``group`` is set).
+
+        bits    : packed tx bytes of the whole run (reference mode) or None (Philox)
+        normals : (nr, ni) float64 arrays of length n_sym*(N+cp) (reference mode), or None
+                  for Philox noise
+        events  : if a list, (kernel, n_symbols, start, end) HIP events are appended around
+                  every ofdm_tx / ofdm_rx launch (recorded on the launch stream)
+        """
+        dev = B.device()
+        stream = B.stream_ptr()
+        world, rank = 1, 0
+        if group is not None:
+            import torch.distributed as dist
+
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+        lo, hi = shard(n_sym, rank, world)
+        mine = hi - lo
+        N, cp = self.n_fft, self.cp
+        samples = n_sym * (N + cp)
+        n_valid = self.valid_bits(n_sym) if n_valid_bits is None else int(n_valid_bits)
+
+        bits_d = None
+        if bits is not None:
+            need = math.ceil(n_sym * self.bps / 8)
+            if len(bits) < need:
+                raise ValueError(f"need {need} tx bytes for {n_sym} OFDM symbols, got {len(bits)}")
+            bits_d = B.to_device(np.asarray(bits, dtype=np.uint8)[: math.ceil(hi * self.bps / 8) + 1])
+        nr_d = ni_d = None
+        if normals is not None and noise_on:
+            nr_d = B.to_device(np.asarray(normals[0], np.float64))
+            ni_d = B.to_device(np.asarray(normals[1], np.float64))
+
+        stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        counters = torch.zeros(2, dtype=torch.int64, device=dev)
+        csize = 8 if self.cdtype == torch.complex64 else 16
+        per_batch = batch or max(1, min(mine, y_budget // (N * csize)))
+        keep = min(keep_symbols, mine)
+        z_out = torch.empty((keep, N), dtype=self.cdtype, device=dev) if keep else None
+
+        def reduce_stats():
+            if world > 1:
+                import torch.distributed as dist
+
+                s01 = stats[:2].clone()
+                dist.all_reduce(s01, op=dist.ReduceOp.SUM, group=group)
+                pk = stats[2:].clone()
+                dist.all_reduce(pk, op=dist.ReduceOp.MAX, group=group)
+                stats[:2].copy_(s01)
+                stats[2:].copy_(pk)
+
+        if per_batch >= mine:
+            # whole shard resident: one TX, one RX
+            y = torch.empty((max(mine, 1), N), dtype=self.cdtype, device=dev)
+            self._timed(events, "ofdm_tx", mine, lambda: self.tx(stream, bits_d, seed, lo, mine, y, stats))
+            reduce_stats()
+            self._timed(events, "ofdm_rx", mine, lambda: self.rx(
+                stream, y, nr_d, ni_d, seed, stats, samples, snr_db, noise_on, bits_d, lo, mine, n_valid,
+                counters, z_out, keep))
+        else:
+            # power pass first (the AWGN power is a whole-stream mean), then TX+RX per batch
+            self.tx(stream, bits_d, seed, lo, mine, None, stats)
+            reduce_stats()
+            scratch = torch.zeros(3, dtype=torch.float64, device=dev)
+            y = torch.empty((per_batch, N), dtype=self.cdtype, device=dev)
+            for b0 in range(lo, hi, per_batch):
+                nb = min(per_batch, hi - b0)
+                self.tx(stream, bits_d, seed, b0, nb, y, scratch)
+                zk = keep if b0 == lo else 0
+                self.rx(stream, y, nr_d, ni_d, seed, stats, samples, snr_db, noise_on, bits_d, b0, nb,
+                        n_valid, counters, z_out if zk else None, zk)
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
+        st = stats.cpu().numpy()
+        cnt = counters.cpu().numpy()
+        avg = st[1] / samples if samples else 0.0
+        papr = float(10 * np.log10(st[2] / avg)) if avg > 0 else float("inf")
+        return LinkStats(
+            bit_errors=int(cnt[0]), symbol_errors=int(cnt[1]), num_ofdm_symbols=n_sym,
+            power_sum=float(st[0]), x_power_sum=float(st[1]), x_peak=float(st[2]), samples=samples,
+            papr_db=papr, received=None if z_out is None else z_out.cpu().numpy().reshape(-1),
+        )
