@@ -192,8 +192,6 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
     if (d->precision != OFDM_F32 && d->precision != OFDM_F64) return fail(OFDM_E_INVALID, "bad precision");
     if (d->equalizer < 0 || d->equalizer > 2) return fail(OFDM_E_INVALID, "bad equalizer");
     if (d->n_taps < 0 || d->n_taps > kMaxTaps) return fail(OFDM_E_INVALID, "n_taps must be in [0, 32]");
-    if (d->n_taps > 1 && d->n_taps - 1 > d->n_fft)
-        return fail(OFDM_E_INVALID, "channel order must not exceed n_fft");
     if (d->n_luts < 0 || d->n_luts > 4) return fail(OFDM_E_INVALID, "n_luts must be in [0, 4]");
 
     ofdm_plan_s* p = new ofdm_plan_s();
@@ -299,6 +297,7 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
             DevBuf hr;
             std::vector<double> hv(d->h_raw, d->h_raw + 2 * d->n_taps);
             if ((rc = upload(hr, hv.data(), hv.size(), s))) return rc;
+            (void)hipGetLastError();
             hipLaunchKernelGGL(k_taps_dft, dim3((p->n + 255) / 256), dim3(256), 0, s, (const double*)hr.p,
                                d->n_taps, p->n, (double*)p->H64.p);
             HIPCHK(hipGetLastError());
@@ -570,6 +569,7 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
     if (!p || !p->has_const || p->L < 1) return fail(OFDM_E_INVALID, "ofdm_tx needs a constellation and channel taps");
     if (!p->separable) return fail(OFDM_E_INVALID, "fused path needs square-QAM constellations");
     if (p->zp) return fail(OFDM_E_INVALID, "fused path supports the cyclic prefix only");
+    if (p->L - 1 > p->n) return fail(OFDM_E_INVALID, "fused path needs channel order <= n_fft");
     if (n_sym < 0 || sym0 < 0 || !stats) return fail(OFDM_E_INVALID, "bad argument to ofdm_tx");
     if (n_sym == 0) return OFDM_OK;
     TxArgs a{};

@@ -386,7 +386,8 @@ __global__ __launch_bounds__(kBlock) void k_tx(TxArgs a) {
     C* h = cv.take<C>(32);
     AxisInfo* axis = cv.take<AxisInfo>(4);
     C* data = cv.take<C>((size_t)G::SPB * G::PADN);
-    C* tail = cv.take<C>((size_t)G::SPB * 32);
+    const int tls = a.L > 1 ? a.L - 1 : 1;  // tail slots per symbol group
+    C* tail = cv.take<C>((size_t)G::SPB * tls);
     const int nbl = cm.bytes_per_sym_lds;
     uint8_t* bitsl = cv.take<uint8_t>((size_t)G::SPB * nbl);
     double* red = cv.take<double>(kBlock / 64);
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(kBlock) void k_tx(TxArgs a) {
 
     const int ls = threadIdx.x / G::TPS, t = threadIdx.x % G::TPS;
     C* buf = data + ls * G::PADN;
-    C* tl = tail + ls * 32;
+    C* tl = tail + ls * tls;
     uint8_t* lb = bitsl + ls * nbl;
     C* yout = (C*)a.y;
     const int cp = cm.cp, L = a.L;
@@ -462,11 +463,11 @@ __global__ __launch_bounds__(kBlock) void k_tx(TxArgs a) {
                 }
             }
             __syncthreads();
-            if (L > 1 && t < L - 1) {
-                // tail for the next symbol: last L-1 samples of this symbol's stream
-                // (host guarantees L-1 <= N); the stream starts with zeros (sg < 0)
-                const int m = G::N + cp - (L - 1) + t;
-                tl[t] = active ? buf[pad(m < cp ? G::N - cp + m : m - cp)] : mk<R>(0, 0);
+            // tail for the next symbol: last L-1 samples of this symbol's stream
+            // (host guarantees L-1 <= N); the stream starts with zeros (sg < 0)
+            for (int j = t; j < L - 1; j += G::TPS) {
+                const int m = G::N + cp - (L - 1) + j;
+                tl[j] = active ? buf[pad(m < cp ? G::N - cp + m : m - cp)] : mk<R>(0, 0);
             }
             __syncthreads();
         }

@@ -8,6 +8,7 @@ OFDM_INSTANTIATE(double)
 
 hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int max_mask,
                            double* stats, hipStream_t s) {
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, s, partials, nblocks, nfields, max_mask, stats);
     return hipGetLastError();
 }
@@ -15,6 +16,7 @@ hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int
 hipError_t launch_nn_classify(const double* lut, int m, const double* z, int64_t n, int64_t* idx,
                               hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_nn_classify, dim3(clamp_grid((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                        lut, m, z, n, idx);
     return hipGetLastError();

@@ -15,8 +15,11 @@ namespace ofdm {
 template <typename F>
 static hipError_t set_smem(F fn, size_t bytes) {
     // Dynamic LDS above 64 KiB must be opted in per kernel; idempotent and cheap.
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    (void)hipGetLastError();  // drop a stale error of an earlier, already-reported call
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) (void)hipGetLastError();
+    return e;
 }
 
 static inline int clamp_grid(int64_t want) {
@@ -53,6 +56,7 @@ hipError_t launch_rows(int logn, int mode, const RowsArgs& a, hipStream_t s) {
 template <typename R>
 hipError_t launch_equalize(const EqArgs& a, hipStream_t s) {
     if (a.n_rows <= 0) return hipSuccess;
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_equalize<R>, dim3(clamp_grid(a.n_rows)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
@@ -60,6 +64,7 @@ hipError_t launch_equalize(const EqArgs& a, hipStream_t s) {
 template <typename R>
 hipError_t launch_map(const MapArgs& a, hipStream_t s) {
     if (a.n_out <= 0) return hipSuccess;
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_map<R>, dim3(clamp_grid((a.n_out + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
@@ -67,18 +72,21 @@ hipError_t launch_map(const MapArgs& a, hipStream_t s) {
 template <typename R>
 hipError_t launch_demap(const DemapArgs& a, hipStream_t s) {
     if (a.n_bytes <= 0) return hipSuccess;
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_demap<R>, dim3(clamp_grid((a.n_bytes + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
 template <typename R>
 hipError_t launch_conv(const ConvArgs& a, int grid, hipStream_t s) {
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_conv<R>, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
 template <typename R>
 hipError_t launch_power(const PowerArgs& a, int grid, hipStream_t s) {
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_power<R>, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
@@ -86,13 +94,14 @@ hipError_t launch_power(const PowerArgs& a, int grid, hipStream_t s) {
 template <typename R>
 hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
     if (a.len <= 0) return hipSuccess;
+    (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_awgn<R>, dim3(clamp_grid((a.len + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int grid, hipStream_t s) {
-    const size_t sm = smem_tx<R>(LOGN, a.c.lut_len, a.c.bytes_per_sym_lds);
+    const size_t sm = smem_tx<R>(LOGN, a.c.lut_len, a.c.bytes_per_sym_lds, a.L);
     auto fn = k_tx<R, LOGN>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;

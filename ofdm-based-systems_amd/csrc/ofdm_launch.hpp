@@ -139,11 +139,12 @@ inline size_t smem_rows(int logn) {
            rnd16(256 * sizeof(R));
 }
 template <typename R>
-inline size_t smem_tx(int logn, int lut_len, int nbl) {
+inline size_t smem_tx(int logn, int lut_len, int nbl, int L) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn);
+    const int tls = L > 1 ? L - 1 : 1;
     return rnd16(128 * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(4 * sizeof(AxisInfo)) +
-           rnd16((size_t)spb * geo_padn(logn) * c) + rnd16((size_t)spb * 32 * c) +
+           rnd16((size_t)spb * geo_padn(logn) * c) + rnd16((size_t)spb * tls * c) +
            rnd16((size_t)spb * nbl) + rnd16(4 * sizeof(double));
 }
 template <typename R>
