@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -161,16 +162,22 @@ int build_axis(const double* lut, int m, int lut_off, AxisInfo& ax) {
     return OFDM_OK;
 }
 
+// Diagnostic ablation switches for timing studies (tools/ablate.py); unset = 0 = normal run.
+int env_flags(const char* name) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : 0;
+}
+
 int log2_exact(int n) {
     int l = 0;
     while ((1 << l) < n) ++l;
     return (1 << l) == n ? l : -1;
 }
 
-// Bytes of one OFDM symbol's bit stream staged in LDS, incl. a <8-bit misalignment
-// of the symbol start and one byte of slack for the 16-bit extraction window; a
-// multiple of 16 so Philox blocks (16 bytes) fit.
-int lds_bytes_per_sym(int bps) { return (int)rnd16((size_t)(bps + 7) / 8 + 2 + 16); }
+// 32-bit words of one OFDM symbol's bit stream staged in LDS: the stream plus a <8-bit
+// misalignment of the symbol start, one slack word for the 64-bit extraction window,
+// rounded up to whole Philox blocks (4 words).
+int lds_words_per_sym(int bps) { return (((bps + 7 + 31) / 32 + 1) + 3) & ~3; }
 
 }  // namespace
 
@@ -557,7 +564,7 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
     c.bps = p->bps;
     c.cp = p->cp;
     c.eq = p->eq;
-    c.bytes_per_sym_lds = lds_bytes_per_sym(p->bps);
+    c.words_per_sym = lds_words_per_sym(p->bps);
     c.scale = 1.0 / std::sqrt((double)p->n);
     c.gain_mean = p->gain_mean;
     c.eq_a = p->eq_a.p;
@@ -579,7 +586,9 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
     a.partials = (double*)p->ws.p;
     a.h = p->h.p;
     a.L = p->L;
-    a.chunk = p->L > 1 ? 8 : 1;
+    a.chunk = p->L > 1 ? 16 : 1;
+    a.slot = tx_slot(p->logn, p->cp, p->L);
+    a.flags = env_flags("OFDM_ABLATE_TX");
     const int spb = geo_spb(p->logn);
     const int64_t groups = (n_sym + a.chunk - 1) / a.chunk;
     const int64_t iters = (groups + spb - 1) / spb;
@@ -615,6 +624,7 @@ int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const 
     a.counters = counters;
     a.z_out = z_out;
     a.z_keep = z_out ? z_keep : 0;
+    a.flags = env_flags("OFDM_ABLATE_RX");
     const int spb = geo_spb(p->logn);
     const int64_t iters = (n_sym + spb - 1) / spb;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(iters, kMaxGrid));

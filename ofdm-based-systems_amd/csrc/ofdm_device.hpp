@@ -243,6 +243,155 @@ __device__ __forceinline__ void load_twiddles(cpx<R>* lds, const cpx<R>* g) {
     if (threadIdx.x < 128) lds[threadIdx.x] = g[threadIdx.x];
 }
 
+// Per-LUT decision info for the separable square-QAM LUTs: LUT[i] = lev[ki] + j lev[kq]
+// with i = (qpat[kq] << hbits) | ipat[ki]; levels sorted ascending, uniform step.
+struct AxisInfo {
+    double lev0;      // most negative level
+    double inv_step;  // 1 / level spacing
+    int32_t side;     // sqrt(M)
+    int32_t hbits;    // b / 2
+    int32_t lut_off;  // offset of this LUT in the pool
+    int32_t bits;     // b
+    uint8_t ipat[16];
+    uint8_t qpat[16];
+};
+
+// Per-subcarrier table for adaptive bit loading.
+struct ScInfo {
+    int16_t lut;     // AxisInfo index, -1 = inactive
+    int16_t bits;    // b_k
+    int32_t bitoff;  // bit offset of subcarrier k inside one OFDM symbol's bit stream
+};
+
+// ------------------------------------------------------------------ register-resident FFT
+// Synchronisation of one symbol group.  When a symbol's TPS threads sit in one
+// wavefront (TPS <= 64) and every LDS region they touch is private to that symbol,
+// a wavefront-scope fence is enough: a wave's LDS operations execute in program
+// order, the fence only stops the compiler from moving them.  Larger groups span
+// waves and need the workgroup barrier (then every thread of the block calls it).
+template <int TPS>
+__device__ __forceinline__ void sym_sync() {
+    if constexpr (TPS <= 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
+// One Stockham pass with the data distribution "thread t owns elements t + i*TPS".
+// FIRST: inputs come from x[] (valid because the first pass has RAD = E, STRIDE = TPS);
+// LAST: outputs stay in x[] (the last pass writes j + r*NS with j = t + q*TPS and
+// NS = TPS*E/RAD, i.e. element t + (q + r*NB)*TPS); otherwise through the LDS row.
+template <typename R, int LOGN, int LOGR, int LOGNS, bool INV, bool FIRST, bool LAST>
+__device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, const cpx<R>* lo,
+                                         const cpx<R>* hi, int t) {
+    using G = Geo<LOGN>;
+    constexpr int RAD = 1 << LOGR;
+    constexpr int NS = 1 << LOGNS;
+    constexpr int NB = G::E / RAD;
+    constexpr int STRIDE = G::N / RAD;
+    cpx<R> v[NB][RAD];
+    if constexpr (FIRST) {
+        static_assert(NB == 1 && STRIDE == G::TPS, "first pass consumes the register layout");
+#pragma unroll
+        for (int r = 0; r < RAD; ++r) v[0][r] = x[r];
+    } else {
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int r = 0; r < RAD; ++r) v[q][r] = buf[pad(t + q * G::TPS + r * STRIDE)];
+        if constexpr (!LAST) sym_sync<G::TPS>();  // every read done before the rewrite
+    }
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        const int j = t + q * G::TPS;
+        const int k = j & (NS - 1);
+        if constexpr (LOGNS > 0) {
+            // w^r by recurrence from one table lookup: 2 live registers instead of the
+            // RAD-1 hoisted table loads (<= 15 roundings: ~1e-6 in f32, ~2e-15 in f64)
+            const cpx<R> w1 = twiddle<R, LOGN, INV>(k << (LOGN - LOGNS - LOGR), lo, hi);
+            cpx<R> wr = w1;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) {
+                v[q][r] = cmul(v[q][r], wr);
+                if (r + 1 < RAD) wr = cmul(wr, w1);
+            }
+        }
+        dft<R, RAD, INV>(v[q]);
+        if constexpr (LAST) {
+#pragma unroll
+            for (int r = 0; r < RAD; ++r) x[q + r * NB] = v[q][r];
+        } else {
+            const int idx = ((j >> LOGNS) << (LOGNS + LOGR)) + k;
+#pragma unroll
+            for (int r = 0; r < RAD; ++r) buf[pad(idx + r * NS)] = v[q][r];
+        }
+    }
+    if constexpr (!LAST) sym_sync<G::TPS>();
+}
+
+template <typename R, int LOGN, int LOGNS, bool INV>
+__device__ __forceinline__ void reg_passes(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, const cpx<R>* lo,
+                                           const cpx<R>* hi, int t) {
+    if constexpr (LOGNS < LOGN) {
+        constexpr int REM = LOGN - LOGNS;
+        constexpr int LOGR = REM >= 4 ? 4 : REM;
+        reg_pass<R, LOGN, LOGR, LOGNS, INV, LOGNS == 0, LOGNS + LOGR == LOGN>(x, buf, lo, hi, t);
+        reg_passes<R, LOGN, LOGNS + LOGR, INV>(x, buf, lo, hi, t);
+    }
+}
+
+// FFT of one symbol: on entry and exit thread t (of TPS) holds element t + i*TPS in
+// x[i].  Unnormalised.  buf is the symbol's private padded LDS row; the caller must
+// sym_sync() between an earlier use of buf and this call when TPS > 64.
+template <typename R, int LOGN, bool INV>
+__device__ __forceinline__ void fft_reg(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, const cpx<R>* lo,
+                                        const cpx<R>* hi, int t) {
+    if constexpr (LOGN <= 4) {
+        dft<R, (1 << LOGN), INV>(x);  // one register-resident pass (TPS = 1)
+    } else {
+        reg_passes<R, LOGN, 0, INV>(x, buf, lo, hi, t);
+    }
+}
+
+// b (<= 8) bits at bit offset o of a stream stored as 32-bit words, stream bit 32w+j
+// = bit (31-j) of word w; one word of slack after the stream.
+__device__ __forceinline__ uint32_t extract_w(const uint32_t* w, int o, int b) {
+    const int q = o >> 5, s = o & 31;
+    const uint64_t x = ((uint64_t)w[q] << 32) | (uint64_t)w[q + 1];
+    return (uint32_t)(x >> (64 - s - b)) & ((1u << b) - 1u);
+}
+
+// Per-axis decision held in registers: ipat / qpat as 4-bit nibbles of a 64-bit word.
+template <typename R>
+struct Slicer {
+    R lev0, inv_step;
+    int smax, hbits;
+    uint64_t ipat, qpat;
+    __device__ void load(const AxisInfo& a) {
+        lev0 = (R)a.lev0;
+        inv_step = (R)a.inv_step;
+        smax = a.side - 1;
+        hbits = a.hbits;
+        ipat = qpat = 0;
+        for (int k = 0; k < a.side; ++k) {
+            ipat |= (uint64_t)a.ipat[k] << (4 * k);
+            qpat |= (uint64_t)a.qpat[k] << (4 * k);
+        }
+    }
+    __device__ __forceinline__ int level(R u) const {
+        int k = (int)floor((u - lev0) * inv_step + (R)0.5);
+        return min(max(k, 0), smax);
+    }
+    __device__ __forceinline__ uint32_t operator()(cpx<R> z) const {
+        const uint32_t i = (uint32_t)(ipat >> (4 * level(z.re))) & 15u;
+        const uint32_t q = (uint32_t)(qpat >> (4 * level(z.im))) & 15u;
+        return (q << hbits) | i;
+    }
+};
+
 // ------------------------------------------------------------------ reductions
 // Sum over the TPS threads of one symbol group (t = threadIdx.x % TPS).  All threads
 // of the workgroup must call it (uses a workgroup barrier for TPS > 64).
@@ -357,26 +506,6 @@ __device__ __forceinline__ void philox_noise_pair(uint64_t seed, int64_t s, uint
 }
 
 // ------------------------------------------------------------------ constellation tables
-// Per-LUT decision info for the separable square-QAM LUTs: LUT[i] = lev[ki] + j lev[kq]
-// with i = (qpat[kq] << hbits) | ipat[ki]; levels sorted ascending, uniform step.
-struct AxisInfo {
-    double lev0;      // most negative level
-    double inv_step;  // 1 / level spacing
-    int32_t side;     // sqrt(M)
-    int32_t hbits;    // b / 2
-    int32_t lut_off;  // offset of this LUT in the pool
-    int32_t bits;     // b
-    uint8_t ipat[16];
-    uint8_t qpat[16];
-};
-
-// Per-subcarrier table for adaptive bit loading.
-struct ScInfo {
-    int16_t lut;     // AxisInfo index, -1 = inactive
-    int16_t bits;    // b_k
-    int32_t bitoff;  // bit offset of subcarrier k inside one OFDM symbol's bit stream
-};
-
 template <typename R>
 __device__ __forceinline__ int slice_axis(R u, const AxisInfo& a) {
     R t = (u - (R)a.lev0) * (R)a.inv_step + (R)0.5;

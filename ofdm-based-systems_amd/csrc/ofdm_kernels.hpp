@@ -342,285 +342,6 @@ __global__ __launch_bounds__(kBlock) void k_nn_classify(const double* lut, int m
 
 #endif  // OFDM_SUPPORT_KERNELS
 
-// ============================================================ fused TX
-// Each symbol group (TPS threads) walks `chunk` consecutive OFDM symbols so the FIR
-// tail (last L-1 samples of the previous symbol) is carried in LDS; the first symbol
-// of a chunk regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
-template <typename R>
-__device__ __forceinline__ void stage_bits(const TxRxCommon& a, int64_t s_global, uint8_t* lb,
-                                           int nbytes_lds, int t, int tps, int& base_bit) {
-    if (a.bits) {
-        const int64_t bit0 = s_global * a.bps;
-        const int64_t B0 = bit0 >> 3;
-        base_bit = (int)(bit0 & 7);
-        const int64_t total_bytes = a.n_bytes;
-        for (int i = t; i < nbytes_lds; i += tps) {
-            const int64_t B = B0 + i;
-            lb[i] = (s_global >= 0 && B < total_bytes) ? a.bits[B] : (uint8_t)0;
-        }
-    } else {
-        base_bit = 0;
-        const int nblk = (a.bps + 127) >> 7;
-        for (int blk = t; blk < nblk; blk += tps) {
-            const u4 o = philox_bits_block(a.seed, s_global, (uint32_t)blk);
-            const uint32_t w[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int B = (blk * 4 + q) * 4;
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (B + i < nbytes_lds) lb[B + i] = (uint8_t)(w[q] >> (24 - 8 * i));
-            }
-        }
-    }
-}
-
-template <typename R, int LOGN>
-__global__ __launch_bounds__(kBlock) void k_tx(TxArgs a) {
-    using G = Geo<LOGN>;
-    using C = cpx<R>;
-    const TxRxCommon& cm = a.c;
-    Carve cv(ofdm_smem);
-    C* tw = cv.take<C>(128);
-    C* lut = cv.take<C>(cm.lut_len);
-    C* h = cv.take<C>(32);
-    AxisInfo* axis = cv.take<AxisInfo>(4);
-    C* data = cv.take<C>((size_t)G::SPB * G::PADN);
-    const int tls = a.L > 1 ? a.L - 1 : 1;  // tail slots per symbol group
-    C* tail = cv.take<C>((size_t)G::SPB * tls);
-    const int nbl = cm.bytes_per_sym_lds;
-    uint8_t* bitsl = cv.take<uint8_t>((size_t)G::SPB * nbl);
-    double* red = cv.take<double>(kBlock / 64);
-
-    load_twiddles<R>(tw, (const C*)cm.tw);
-    for (int i = threadIdx.x; i < cm.lut_len; i += kBlock) lut[i] = ((const C*)cm.lut)[i];
-    if (threadIdx.x < a.L) h[threadIdx.x] = ((const C*)a.h)[threadIdx.x];
-    if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
-    __syncthreads();
-
-    const int ls = threadIdx.x / G::TPS, t = threadIdx.x % G::TPS;
-    C* buf = data + ls * G::PADN;
-    C* tl = tail + ls * tls;
-    uint8_t* lb = bitsl + ls * nbl;
-    C* yout = (C*)a.y;
-    const int cp = cm.cp, L = a.L;
-    const R scale = (R)cm.scale;
-    const int64_t ngroups = (cm.n_sym + a.chunk - 1) / a.chunk;
-    const int64_t niter = (ngroups + G::SPB - 1) / G::SPB;
-    double py = 0, px = 0, mx = 0;
-
-    for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
-        const int64_t grp = it * G::SPB + ls;
-        const int64_t sbeg = grp * a.chunk;  // local symbol index
-        for (int c = (L > 1 ? -1 : 0); c < a.chunk; ++c) {
-            const int64_t sl = sbeg + c;
-            const int64_t sg = cm.sym0 + sl;
-            const bool active = grp < ngroups && sl < cm.n_sym && sg >= 0;
-            int base_bit = 0;
-            if (active) stage_bits<R>(cm, sg, lb, nbl, t, G::TPS, base_bit);
-            __syncthreads();
-            // map (QAMConstellationMapper.encode, constellation/models.py:240-246) with the
-            // ortho 1/sqrt(N) of ifft(norm="ortho") folded in
-#pragma unroll
-            for (int i = 0; i < G::E; ++i) {
-                const int k = t + i * G::TPS;
-                C v = mk<R>(0, 0);
-                if (active) {
-                    if (cm.adaptive) {
-                        const ScInfo sc = cm.sc[k];
-                        if (sc.lut >= 0) {
-                            const uint32_t idx = extract_bits(lb, base_bit + sc.bitoff, sc.bits);
-                            v = lut[axis[sc.lut].lut_off + idx];
-                        }
-                    } else {
-                        v = lut[extract_bits(lb, base_bit + (int64_t)k * cm.b, cm.b)];
-                    }
-                }
-                buf[pad(k)] = cscale(v, scale);
-            }
-            __syncthreads();
-            fft_passes<R, LOGN, 0, true>(buf, tw, tw + 64, t);
-            // x = buf (natural order).  Serial stream of this symbol: ext(m) for
-            // m in [0, N+cp): m < cp -> x[N-cp+m], else x[m-cp]; ext(<0) = previous tail.
-            if (active && c >= 0) {
-                for (int m = t; m < G::N + cp; m += G::TPS) {
-                    C yv = mk<R>(0, 0);
-                    for (int l = 0; l < L; ++l) {
-                        const int q = m - l;
-                        C xv;
-                        if (q < 0)
-                            xv = tl[L - 1 + q];
-                        else
-                            xv = buf[pad(q < cp ? G::N - cp + q : q - cp)];
-                        yv = yv + cmul(h[l], xv);
-                    }
-                    py += (double)norm2(yv);
-                    const C xm = buf[pad(m < cp ? G::N - cp + m : m - cp)];
-                    const double p2 = (double)norm2(xm);
-                    px += p2;
-                    mx = p2 > mx ? p2 : mx;
-                    if (yout && m >= cp) yout[sl * G::N + (m - cp)] = yv;
-                }
-            }
-            __syncthreads();
-            // tail for the next symbol: last L-1 samples of this symbol's stream
-            // (host guarantees L-1 <= N); the stream starts with zeros (sg < 0)
-            for (int j = t; j < L - 1; j += G::TPS) {
-                const int m = G::N + cp - (L - 1) + j;
-                tl[j] = active ? buf[pad(m < cp ? G::N - cp + m : m - cp)] : mk<R>(0, 0);
-            }
-            __syncthreads();
-        }
-    }
-    py = block_sum<double>(py, red);
-    px = block_sum<double>(px, red);
-    mx = block_max<double>(mx, red);
-    if (threadIdx.x == 0) {
-        a.partials[blockIdx.x * 3 + 0] = py;
-        a.partials[blockIdx.x * 3 + 1] = px;
-        a.partials[blockIdx.x * 3 + 2] = mx;
-    }
-}
-
-// ============================================================ fused RX
-template <typename R, int LOGN>
-__global__ __launch_bounds__(kBlock) void k_rx(RxArgs a) {
-    using G = Geo<LOGN>;
-    using C = cpx<R>;
-    const TxRxCommon& cm = a.c;
-    Carve cv(ofdm_smem);
-    C* tw = cv.take<C>(128);
-    AxisInfo* axis = cv.take<AxisInfo>(4);
-    C* data = cv.take<C>((size_t)G::SPB * G::PADN);
-    const int nbl = cm.bytes_per_sym_lds;
-    uint8_t* bitsl = cv.take<uint8_t>((size_t)G::SPB * nbl);
-    R* red = cv.take<R>(kBlock);
-    double* redd = cv.take<double>(kBlock / 64);
-
-    load_twiddles<R>(tw, (const C*)cm.tw);
-    if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
-    __syncthreads();
-
-    const int ls = threadIdx.x / G::TPS, t = threadIdx.x % G::TPS;
-    C* buf = data + ls * G::PADN;
-    uint8_t* lb = bitsl + ls * nbl;
-    const C* yin = (const C*)a.y;
-    const int cp = cm.cp;
-    const R scale = (R)cm.scale;
-
-    // sigma from the whole-stream mean power (noise/models.py:13-22)
-    R sigma = 0;
-    if (a.noise_on) {
-        const double p = a.stats[0] / (double)a.total_samples;
-        sigma = (R)sqrt((p / a.snr_lin) / 2.0);
-    }
-    const int64_t niter = (cm.n_sym + G::SPB - 1) / G::SPB;
-    uint64_t be = 0, se = 0;
-
-    for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
-        const int64_t sl = it * G::SPB + ls;
-        const int64_t sg = cm.sym0 + sl;
-        const bool active = sl < cm.n_sym;
-        int base_bit = 0;
-        if (active) stage_bits<R>(cm, sg, lb, nbl, t, G::TPS, base_bit);
-        // load kept samples + AWGN, ortho scale folded in
-        if (a.nr) {
-#pragma unroll
-            for (int i = 0; i < G::E; ++i) {
-                const int k = t + i * G::TPS;
-                C v = mk<R>(0, 0);
-                if (active) {
-                    v = yin[sl * G::N + k];
-                    if (a.noise_on) {
-                        const int64_t gi = sg * (G::N + cp) + cp + k;
-                        v.re += sigma * (R)a.nr[gi];
-                        v.im += sigma * (R)a.ni[gi];
-                    }
-                }
-                buf[pad(k)] = cscale(v, scale);
-            }
-        } else {
-            // Philox noise: thread owns sample pairs (2p, 2p+1)
-#pragma unroll
-            for (int i = 0; i < (G::E + 1) / 2; ++i) {
-                const int p = t + i * G::TPS;
-                if (2 * p >= G::N) break;
-                C v0 = mk<R>(0, 0), v1 = mk<R>(0, 0);
-                if (active) {
-                    v0 = yin[sl * G::N + 2 * p];
-                    if (2 * p + 1 < G::N) v1 = yin[sl * G::N + 2 * p + 1];
-                    if (a.noise_on) {
-                        float r0, i0, r1, i1;
-                        philox_noise_pair(cm.seed, sg, (uint32_t)p, r0, i0, r1, i1);
-                        v0.re += sigma * (R)r0;
-                        v0.im += sigma * (R)i0;
-                        v1.re += sigma * (R)r1;
-                        v1.im += sigma * (R)i1;
-                    }
-                }
-                buf[pad(2 * p)] = cscale(v0, scale);
-                if (2 * p + 1 < G::N) buf[pad(2 * p + 1)] = cscale(v1, scale);
-            }
-        }
-        __syncthreads();
-        fft_passes<R, LOGN, 0, false>(buf, tw, tw + 64, t);
-        // MMSE noise variance per OFDM symbol (equalization/models.py:39-49)
-        R nv = 0;
-        if (cm.eq == OFDM_EQ_MMSE) {
-            R p = 0;
-#pragma unroll
-            for (int i = 0; i < G::E; ++i) p += norm2(buf[pad(t + i * G::TPS)]);
-            p = group_sum<R, G::TPS>(p, red);
-            nv = cm.gain_mean == 0.0 ? (R)INFINITY : ((p / (R)G::N) / (R)a.snr_lin) / (R)cm.gain_mean;
-        }
-        if (active) {
-            const int64_t sbit = sg * cm.bps;
-            const bool all_valid = sbit + cm.bps <= a.n_valid_bits;
-#pragma unroll
-            for (int i = 0; i < G::E; ++i) {
-                const int k = t + i * G::TPS;
-                C v = buf[pad(k)];
-                if (cm.eq == OFDM_EQ_ZF) {
-                    v = cmul(v, ((const C*)cm.eq_a)[k]);
-                } else if (cm.eq == OFDM_EQ_MMSE) {
-                    const C hc = ((const C*)cm.eq_a)[k];
-                    const R d = ((const R*)cm.eq_b)[k] + nv;
-                    v = cmul(v, mk<R>(hc.re / d, hc.im / d));
-                }
-                if (sl < a.z_keep) ((C*)a.z_out)[sl * G::N + k] = v;
-                int b, off, ai;
-                if (cm.adaptive) {
-                    const ScInfo sc = cm.sc[k];
-                    if (sc.lut < 0) continue;
-                    b = sc.bits;
-                    off = sc.bitoff;
-                    ai = sc.lut;
-                } else {
-                    b = cm.b;
-                    off = k * cm.b;
-                    ai = 0;
-                }
-                const uint32_t ridx = slice<R>(v, axis[ai]);
-                const uint32_t tidx = extract_bits(lb, base_bit + off, b);
-                uint32_t d = ridx ^ tidx;
-                se += d != 0u;
-                if (!all_valid) {
-                    const int64_t nv_bits = a.n_valid_bits - (sbit + off);
-                    const int keep = nv_bits <= 0 ? 0 : (nv_bits >= b ? b : (int)nv_bits);
-                    d &= ((1u << keep) - 1u) << (b - keep);
-                }
-                be += __popc(d);
-            }
-        }
-        __syncthreads();
-    }
-    unsigned long long fb = be, fs = se;
-    fb = block_sum<unsigned long long>(fb, (unsigned long long*)redd);
-    fs = block_sum<unsigned long long>(fs, (unsigned long long*)redd);
-    if (threadIdx.x == 0) {
-        if (fb) atomicAdd((unsigned long long*)&a.counters[0], fb);
-        if (fs) atomicAdd((unsigned long long*)&a.counters[1], fs);
-    }
-}
-
 }  // namespace ofdm
+
+#include "ofdm_fused.hpp"

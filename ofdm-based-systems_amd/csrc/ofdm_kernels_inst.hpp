@@ -101,7 +101,7 @@ hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
 
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int grid, hipStream_t s) {
-    const size_t sm = smem_tx<R>(LOGN, a.c.lut_len, a.c.bytes_per_sym_lds, a.L);
+    const size_t sm = smem_tx<R>(LOGN, a.c.lut_len, a.c.words_per_sym, a.L, a.c.cp);
     auto fn = k_tx<R, LOGN>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
@@ -122,14 +122,28 @@ hipError_t launch_tx(int logn, const TxArgs& a, int grid, hipStream_t s) {
 #undef OFDM_TX_CASE
 }
 
-template <typename R, int LOGN>
-static hipError_t rx_one(const RxArgs& a, int grid, hipStream_t s) {
-    const size_t sm = smem_rx<R>(LOGN, a.c.bytes_per_sym_lds);
-    auto fn = k_rx<R, LOGN>;
+template <typename R, int LOGN, int EQ, bool FAST>
+static hipError_t rx_launch(const RxArgs& a, int grid, hipStream_t s) {
+    const size_t sm = smem_rx<R>(LOGN, a.c.words_per_sym);
+    auto fn = k_rx<R, LOGN, EQ, FAST>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), sm, s, a);
     return hipGetLastError();
+}
+
+// Throughput configuration (complex64, fixed QAM, Philox bits + noise) -> specialised
+// kernel with the equaliser compiled in; anything else -> the generic kernel.
+template <typename R, int LOGN>
+static hipError_t rx_one(const RxArgs& a, int grid, hipStream_t s) {
+    const bool fast = sizeof(R) == 4 && !a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr &&
+                      a.z_out == nullptr;
+    if (fast) {
+        if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, true>(a, grid, s);
+        if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, true>(a, grid, s);
+        return rx_launch<R, LOGN, OFDM_EQ_MMSE, true>(a, grid, s);
+    }
+    return rx_launch<R, LOGN, -1, false>(a, grid, s);
 }
 
 template <typename R>

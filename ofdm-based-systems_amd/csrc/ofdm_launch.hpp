@@ -93,7 +93,7 @@ struct TxRxCommon {
     int n_axis;
     const ScInfo* sc;
     int adaptive, b, bps, cp, eq;
-    int bytes_per_sym_lds;
+    int words_per_sym;  // LDS words staged per OFDM symbol (stream + misalignment + slack)
     double scale, gain_mean;
     const void* eq_a;
     const void* eq_b;
@@ -106,6 +106,8 @@ struct TxArgs {
     const void* h;
     int L;
     int chunk;
+    int slot;   // complex elements per symbol row in LDS
+    int flags;  // diagnostic ablation (OFDM_ABLATE_TX): 1 no bit staging, 2 no FFT, 4 no y store
 };
 
 struct RxArgs {
@@ -121,6 +123,8 @@ struct RxArgs {
     uint64_t* counters;
     void* z_out;
     int64_t z_keep;
+    int flags;  // diagnostic ablation (OFDM_ABLATE_RX): 1 no noise, 2 no FFT, 4 no bit staging,
+                // 8 no equalise/demap/compare, 16 no y load
 };
 
 // ---- LDS footprints (must mirror the Carve sequences in ofdm_kernels.hpp)
@@ -138,21 +142,25 @@ inline size_t smem_rows(int logn) {
     return rnd16(128 * c) + rnd16((size_t)spb * geo_padn(logn) * c) + rnd16(spb * sizeof(R)) +
            rnd16(256 * sizeof(R));
 }
+inline int tx_slot(int logn, int cp, int L) {
+    const int ext = (1 << logn) + cp + (L > 1 ? L - 1 : 0);
+    return geo_padn(logn) > ext ? geo_padn(logn) : ext;
+}
 template <typename R>
-inline size_t smem_tx(int logn, int lut_len, int nbl, int L) {
+inline size_t smem_tx(int logn, int lut_len, int wps, int L, int cp) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn);
     const int tls = L > 1 ? L - 1 : 1;
     return rnd16(128 * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(4 * sizeof(AxisInfo)) +
-           rnd16((size_t)spb * geo_padn(logn) * c) + rnd16((size_t)spb * tls * c) +
-           rnd16((size_t)spb * nbl) + rnd16(4 * sizeof(double));
+           rnd16((size_t)spb * tx_slot(logn, cp, L) * c) + rnd16((size_t)spb * tls * c) +
+           rnd16((size_t)spb * wps * 4) + rnd16(4 * sizeof(double));
 }
 template <typename R>
-inline size_t smem_rx(int logn, int nbl) {
+inline size_t smem_rx(int logn, int wps) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn);
     return rnd16(128 * c) + rnd16(4 * sizeof(AxisInfo)) + rnd16((size_t)spb * geo_padn(logn) * c) +
-           rnd16((size_t)spb * nbl) + rnd16(256 * sizeof(R)) + rnd16(4 * sizeof(double));
+           rnd16((size_t)spb * wps * 4) + rnd16(256 * sizeof(R)) + rnd16(4 * sizeof(unsigned long long));
 }
 
 // ---- launchers (instantiated for float and double in ofdm_kernels_f{32,64}.hip)

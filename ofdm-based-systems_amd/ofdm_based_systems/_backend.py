@@ -19,7 +19,11 @@ from typing import Optional
 import numpy as np
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libofdm_hip.so")
+# OFDM_LIB_VARIANT selects an alternative in-tree build (_lib/libofdm_hip_<variant>.so) for
+# A/B timing studies; unset = the production library.
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                         "libofdm_hip%s.so" % ("_" + os.environ["OFDM_LIB_VARIANT"]
+                                               if os.environ.get("OFDM_LIB_VARIANT") else ""))
 ABI_VERSION = 1
 
 OFDM_F32, OFDM_F64 = 0, 1
