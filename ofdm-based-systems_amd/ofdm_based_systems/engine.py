@@ -72,6 +72,15 @@ class LinkEngine:
         self._lib = B.lib()
 
     # ------------------------------------------------------------------ helpers
+    def device(self) -> torch.device:
+        return B.device()
+
+    def stream(self):
+        return B.stream_ptr()
+
+    def upload(self, a: np.ndarray) -> torch.Tensor:
+        return torch.from_numpy(np.ascontiguousarray(a)).to(self.device())
+
     def valid_bits(self, n_sym: int) -> int:
         """Bits the reference compares: all of them in FIXED mode, whole bytes in adaptive mode
         (AdaptiveConstellationMapper.decode drops a partial byte, constellation/adaptive.py:259-263)."""
@@ -112,8 +121,8 @@ class LinkEngine:
         events  : if a list, (kernel, n_symbols, start, end) HIP events are appended around
                   every ofdm_tx / ofdm_rx launch (recorded on the launch stream)
         """
-        dev = B.device()
-        stream = B.stream_ptr()
+        dev = self.device()
+        stream = self.stream()
         world, rank = 1, 0
         if group is not None:
             import torch.distributed as dist
@@ -130,11 +139,11 @@ class LinkEngine:
             need = math.ceil(n_sym * self.bps / 8)
             if len(bits) < need:
                 raise ValueError(f"need {need} tx bytes for {n_sym} OFDM symbols, got {len(bits)}")
-            bits_d = B.to_device(np.asarray(bits, dtype=np.uint8)[: math.ceil(hi * self.bps / 8) + 1])
+            bits_d = self.upload(np.asarray(bits, dtype=np.uint8)[: math.ceil(hi * self.bps / 8) + 1])
         nr_d = ni_d = None
         if normals is not None and noise_on:
-            nr_d = B.to_device(np.asarray(normals[0], np.float64))
-            ni_d = B.to_device(np.asarray(normals[1], np.float64))
+            nr_d = self.upload(np.asarray(normals[0], np.float64))
+            ni_d = self.upload(np.asarray(normals[1], np.float64))
 
         stats = torch.zeros(3, dtype=torch.float64, device=dev)
         counters = torch.zeros(2, dtype=torch.int64, device=dev)

@@ -1,0 +1,133 @@
+"""Multi-rank path of LinkEngine.run on CPU (gloo, world_size 2).
+
+The GPU kernels are replaced by a test double that computes ofdm_tx / ofdm_rx with
+the oracle on CPU tensors; everything else -- the symbol sharding, the all-reduce of
+the AWGN power statistics between TX and RX, the batched power-pass schedule and the
+counter all-reduce -- is the production LinkEngine.run.  The sharded result must equal
+the single-process oracle run bit for bit.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+from conftest import channel
+
+import ofdm_oracle as O
+from ofdm_based_systems.engine import LinkEngine, shard
+
+
+class OracleEngine(LinkEngine):
+    """LinkEngine whose two kernels are computed by the oracle on the CPU (test double)."""
+
+    def __init__(self, N, M, h_raw, cp, eq):
+        self.n_fft, self.cp, self.h, self.eq = N, cp, np.asarray(h_raw, np.complex128), eq
+        self.b = int(np.log2(M))
+        self.bps = N * self.b
+        self.adaptive = False
+        self.cdtype = torch.complex128
+        self.lut = O.qam_lut(M)
+        self.hn = O.normalize_h(self.h)
+        self.H = np.fft.fft(self.h, N)
+
+    def device(self):
+        return torch.device("cpu")
+
+    def stream(self):
+        return None
+
+    def _ext(self, bits, s):
+        """Modulated OFDM symbol s with its prefix (zeros before the stream starts)."""
+        N, cp = self.n_fft, self.cp
+        if s < 0:
+            return np.zeros(N + cp, np.complex128)
+        nb = self.bps // 8
+        raw = bits[s * nb:(s + 1) * nb].numpy().tobytes()
+        X = self.lut[O.bits_to_indices(O.bytes_to_bits(raw), self.b)]
+        return O.add_cp(np.fft.ifft(X[None, :], norm="ortho"), cp)[0]
+
+    def tx(self, stream, bits_d, seed, sym0, n_sym, y, stats):
+        L = len(self.h)
+        for s in range(sym0, sym0 + n_sym):
+            ext = self._ext(bits_d, s)
+            prev = self._ext(bits_d, s - 1)[len(ext) - (L - 1):] if L > 1 else np.zeros(0)
+            full = np.convolve(np.concatenate([prev, ext]), self.hn)[L - 1:L - 1 + len(ext)]
+            stats[0] += float(np.sum(np.abs(full) ** 2))
+            stats[1] += float(np.sum(np.abs(ext) ** 2))
+            stats[2] = max(float(stats[2]), float(np.max(np.abs(ext) ** 2)))
+            if y is not None:
+                y[s - sym0] = torch.from_numpy(full[self.cp:])
+
+    def rx(self, stream, y, nr, ni, seed, stats, total_samples, snr_db, noise_on, bits_d, sym0, n_sym,
+           n_valid, counters, z_out=None, z_keep=0):
+        N, cp = self.n_fft, self.cp
+        sigma = np.sqrt(float(stats[0]) / total_samples / 10 ** (snr_db / 10) / 2) if noise_on else 0.0
+        nb = self.bps // 8
+        for s in range(sym0, sym0 + n_sym):
+            v = y[s - sym0].numpy().copy()
+            if noise_on:
+                g = s * (N + cp) + cp
+                v = v + sigma * (nr[g:g + N].numpy() + 1j * ni[g:g + N].numpy())
+            Z = O.equalize(np.fft.fft(v[None, :], norm="ortho"), self.H, self.eq, snr_db)[0]
+            ridx = O.nn_demap(Z, self.lut)
+            tidx = O.bits_to_indices(O.bytes_to_bits(bits_d[s * nb:(s + 1) * nb].numpy().tobytes()), self.b)
+            d = ridx ^ tidx
+            counters[0] += int(sum(bin(int(x)).count("1") for x in d))
+            counters[1] += int(np.count_nonzero(d))
+
+
+CASE = dict(N=64, M=16, ch="severe_multipath", eq="MMSE", snr=14.0, S=48, seed=5)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, batch, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = CASE
+    h = channel(c["ch"])
+    cp = len(h) - 1
+    b = int(np.log2(c["M"]))
+    tx, nz = O.reference_streams(c["seed"], c["S"] * c["N"] * b, c["S"] * (c["N"] + cp))
+    eng = OracleEngine(c["N"], c["M"], h, cp, c["eq"])
+    st = eng.run(c["S"], c["snr"], bits=np.frombuffer(tx, np.uint8), normals=nz, group=dist.group.WORLD,
+                 batch=batch)
+    out[rank] = (st.bit_errors, st.symbol_errors, st.papr_db, st.power_sum)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch", [(2, None), (2, 5), (3, None)])
+def test_sharded_engine_matches_single_process_oracle(world, batch):
+    c = CASE
+    h = channel(c["ch"])
+    cp = len(h) - 1
+    b = int(np.log2(c["M"]))
+    tx, nz = O.reference_streams(c["seed"], c["S"] * c["N"] * b, c["S"] * (c["N"] + cp))
+    ref = O.run_fixed(tx, c["S"] * c["N"] * b, c["N"], c["M"], h, cp, c["eq"], c["snr"], nz)
+    assert ref.bit_errors > 0
+    out = mp.Manager().dict()
+    mp.spawn(_worker, args=(world, _free_port(), batch, out), nprocs=world, join=True)
+    for r in range(world):
+        be, se, papr, _ = out[r]
+        assert (be, se) == (ref.bit_errors, ref.symbol_errors), (r, be, se, ref)
+        assert abs(papr - ref.papr_db) < 1e-9
+    assert len({out[r][3] for r in range(world)}) == 1  # every rank saw the same global power
+
+
+def test_shard_covers_range_exactly():
+    for n in (0, 1, 7, 100, 1001):
+        for w in (1, 2, 3, 8):
+            parts = [shard(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+            assert max(hi - lo for lo, hi in parts) - min(hi - lo for lo, hi in parts) <= 1
