@@ -505,6 +505,80 @@ __device__ __forceinline__ void philox_noise_pair(uint64_t seed, int64_t s, uint
     i1 = a1 * __builtin_amdgcn_sinf(v1);
 }
 
+// ------------------------------------------------------------------ throughput-mode streams
+// Definition (philox mode): thread t of OFDM symbol s owns elements k = t + TPS*i.
+//  * bits : one Philox4x32-10 block keyed (seed; ctr = t, s, kLaneBits) = 128 bits,
+//           MSB-first; element i takes the next b_k bits in element order.
+//  * noise: xoshiro128** seeded by one Philox4x32-10 block (seed; t, s, kLaneNoise);
+//           element i consumes two outputs (u1, u2) -> Box-Muller -> (re, im).
+// Both depend only on (seed, s, N), so results do not depend on how symbols are
+// batched or sharded across GPUs.
+constexpr uint32_t kLaneBits = 0x1A7EB175u;
+constexpr uint32_t kLaneNoise = 0x1A7E4015u;
+
+__device__ __forceinline__ u4 philox_lane(uint64_t seed, int64_t s, uint32_t t, uint32_t stream) {
+    u4 c;
+    c.x = t;
+    c.y = (uint32_t)s;
+    c.z = (uint32_t)((uint64_t)s >> 32);
+    c.w = stream;
+    return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
+// b bits at compile-time offset O of the 128-bit block w0..w3.
+template <int O, int Bb>
+__device__ __forceinline__ uint32_t bits128_c(const u4& w) {
+    constexpr int q = O >> 5, s = O & 31;
+    const uint32_t a[4] = {w.x, w.y, w.z, w.w};
+    if constexpr (s + Bb <= 32) {
+        return (a[q] >> (32 - s - Bb)) & ((1u << Bb) - 1u);
+    } else {
+        return ((a[q] << (s + Bb - 32)) | (a[q + 1] >> (64 - s - Bb))) & ((1u << Bb) - 1u);
+    }
+}
+
+// b bits at run-time offset o (o + b <= 128).
+__device__ __forceinline__ uint32_t bits128(const u4& w, int o, int b) {
+    const int q = o >> 5, s = o & 31;
+    const uint32_t hi = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+    const uint32_t lo = q == 0 ? w.y : q == 1 ? w.z : q == 2 ? w.w : 0u;
+    const uint64_t x = ((uint64_t)hi << 32) | lo;
+    return (uint32_t)(x >> (64 - s - b)) & ((1u << b) - 1u);
+}
+
+// xoshiro128** (Blackman & Vigna): 4x32-bit state, ~12 simple ALU ops per output.
+struct Xoshiro128ss {
+    uint32_t s0, s1, s2, s3;
+    __device__ __forceinline__ static uint32_t rotl(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+    __device__ __forceinline__ void seed(const u4& v) {
+        s0 = v.x;
+        s1 = v.y;
+        s2 = v.z;
+        s3 = v.w | ((v.x | v.y | v.z) == 0u ? 1u : 0u);  // never the all-zero state
+    }
+    __device__ __forceinline__ uint32_t next() {
+        const uint32_t r = rotl(s1 * 5u, 7) * 9u;
+        const uint32_t t = s1 << 9;
+        s2 ^= s0;
+        s3 ^= s1;
+        s1 ^= s2;
+        s0 ^= s3;
+        s2 ^= t;
+        s3 = rotl(s3, 11);
+        return r;
+    }
+    // one complex standard normal (re, im each N(0,1)) by Box-Muller on the hardware
+    // transcendentals (v_log_f32 = log2, v_sin/cos_f32 take revolutions)
+    __device__ __forceinline__ void normal2(float& re, float& im) {
+        const float k = 2.3283064365386963e-10f;  // 2^-32
+        const float u = ((float)next() + 0.5f) * k;
+        const float v = (float)next() * k;
+        const float a = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u));
+        re = a * __builtin_amdgcn_cosf(v);
+        im = a * __builtin_amdgcn_sinf(v);
+    }
+};
+
 // ------------------------------------------------------------------ constellation tables
 template <typename R>
 __device__ __forceinline__ int slice_axis(R u, const AxisInfo& a) {

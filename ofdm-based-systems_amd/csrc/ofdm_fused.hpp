@@ -4,11 +4,18 @@
 // elements k = t + i*TPS (i < E) in registers from the constellation map through
 // the IFFT to the channel output (TX), and from the HBM load through the FFT to
 // the error count (RX).  LDS carries only the Stockham transposes between FFT
-// passes, the symbol's tx bit words, and (TX, multipath) the extended serial
-// stream for the FIR.  With TPS <= 64 a symbol lives in one wavefront and every
-// synchronisation is wave-local (sym_sync), so the 4 waves of a workgroup run
-// decoupled.
+// passes, (reference mode) the symbol's tx bit words, and (TX, multipath) the
+// extended serial stream for the FIR.  With TPS <= 64 a symbol lives in one
+// wavefront and every synchronisation is wave-local (sym_sync), so the 4 waves of a
+// workgroup run decoupled.
+//
+// Specialisations: FB = 2/4/6/8 selects the throughput kernel (fixed square QAM with
+// b = FB bits, Philox-keyed bits and noise, complex64) with everything else compiled
+// out; FB = 0 is the generic kernel (reference-mode bytes and normals, adaptive bit
+// loading, complex128).
 #pragma once
+
+#include <type_traits>
 
 // Minimum waves per SIMD requested per fused kernel (register budget 512/waves), tuned on
 // MI355X (tools/ab.sh): TX 3 waves/SIMD, RX unconstrained.  Build-time knobs (Makefile
@@ -22,37 +29,23 @@
 
 namespace ofdm {
 
-// Stage OFDM symbol s's tx bit stream as 32-bit words in W (stream bit 32w+j =
-// bit 31-j of word w).  Returns the offset of the symbol's first bit in word 0.
-// Reference mode: the packed bytes of the run (symbol s starts at bit s*bps, zero past
-// the end).  Throughput mode: Philox4x32-10 blocks keyed by (seed, s).
+// Reference mode: stage OFDM symbol s's tx bits from the packed bytes of the run
+// (symbol s starts at bit s*bps, zeros past the end) as 32-bit words in W
+// (stream bit 32w+j = bit 31-j of word w).  Returns the symbol's bit offset in word 0.
 template <int TPS>
 __device__ __forceinline__ int stage_words(const TxRxCommon& a, int64_t s, uint32_t* W, int t) {
-    const int nw = a.words_per_sym;
-    if (a.bits) {
-        const int64_t bit0 = s * a.bps;
-        const int64_t B0 = bit0 >> 3;
-        for (int w = t; w < nw; w += TPS) {
-            uint32_t v = 0;
+    const int64_t bit0 = s * a.bps;
+    const int64_t B0 = bit0 >> 3;
+    for (int w = t; w < a.words_per_sym; w += TPS) {
+        uint32_t v = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int64_t B = B0 + 4 * w + i;
-                v = (v << 8) | (uint32_t)((B < a.n_bytes && s >= 0) ? a.bits[B] : 0);
-            }
-            W[w] = v;
+        for (int i = 0; i < 4; ++i) {
+            const int64_t B = B0 + 4 * w + i;
+            v = (v << 8) | (uint32_t)((B < a.n_bytes && s >= 0) ? a.bits[B] : 0);
         }
-        return (int)(bit0 & 7);
+        W[w] = v;
     }
-    for (int blk = t; blk < (nw >> 2); blk += TPS) {
-        const u4 o = philox_bits_block(a.seed, s, (uint32_t)blk);
-        uint4 v;
-        v.x = o.x;
-        v.y = o.y;
-        v.z = o.z;
-        v.w = o.w;
-        *reinterpret_cast<uint4*>(W + 4 * blk) = v;
-    }
-    return 0;
+    return (int)(bit0 & 7);
 }
 
 template <typename R>
@@ -76,16 +69,58 @@ __device__ __forceinline__ cpx<R> mmse_coef(cpx<R> hc, R h2, R nv) {
     }
 }
 
+// Per-element tx constellation indices of one symbol for this lane, from whichever
+// source the launch uses: the lane's Philox block (philox mode) or the staged words
+// (reference mode).  FB > 0: fixed b = FB, compile-time offsets.
+template <int FB, int TPS>
+struct TxBits {
+    u4 lane;
+    const uint32_t* W;
+    int base_bit;
+    bool from_words;
+
+    __device__ __forceinline__ void load(const TxRxCommon& a, int64_t s, int t, uint32_t* Wslot, bool active) {
+        from_words = FB == 0 && a.bits != nullptr;
+        W = Wslot;
+        base_bit = 0;
+        lane.x = lane.y = lane.z = lane.w = 0u;
+        if (from_words) {
+            if (active) base_bit = stage_words<TPS>(a, s, Wslot, t);
+        } else if (active) {
+            lane = philox_lane(a.seed, s, (uint32_t)t, kLaneBits);
+        }
+    }
+    template <int I>
+    __device__ __forceinline__ uint32_t fixed() const {
+        return bits128_c<FB * I, FB>(lane);
+    }
+    // lane_off: running offset over this lane's active elements (philox mode);
+    // stream_off: the element's offset inside the symbol's stream (reference mode)
+    __device__ __forceinline__ uint32_t generic(int lane_off, int b, int stream_off) const {
+        if (from_words) return extract_w(W, base_bit + stream_off, b);
+        return bits128(lane, lane_off, b);
+    }
+};
+
+template <int I, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < E) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, E>(f);
+    }
+}
+
 // ============================================================ fused TX
 // Each symbol group walks `chunk` consecutive OFDM symbols so the FIR tail (last L-1
 // stream samples of the previous symbol) is carried in LDS; the first symbol of a chunk
 // regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
-template <typename R, int LOGN>
+template <typename R, int LOGN, int FB>
 __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
     using G = Geo<LOGN>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
     const TxRxCommon& cm = a.c;
+    const bool adaptive = FB ? false : (bool)cm.adaptive;
     const int cp = cm.cp, L = a.L;
     const int slot = a.slot;  // complex elements per symbol row (>= PADN and >= L-1+cp+N)
     const int tls = L > 1 ? L - 1 : 1;
@@ -105,7 +140,8 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     __syncthreads();
 
-    const int ls = threadIdx.x / TPS, t = threadIdx.x % TPS;
+    const int ls = TPS >= 64 ? __builtin_amdgcn_readfirstlane(threadIdx.x / TPS) : threadIdx.x / TPS;
+    const int t = threadIdx.x % TPS;
     C* row = rows + ls * slot;
     C* tl = tails + ls * tls;
     uint32_t* W = words + ls * cm.words_per_sym;
@@ -123,25 +159,36 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
             const int64_t sl = sbeg + c;
             const int64_t sg = cm.sym0 + sl;
             const bool active = grp < ngroups && sl < cm.n_sym && sg >= 0;
-            int base_bit = 0;
-            if (active && !(a.flags & 1)) base_bit = stage_words<TPS>(cm, sg, W, t);
-            sym_sync<TPS>();
+            TxBits<FB, TPS> tb;
+            tb.load(cm, sg, t, W, active && !(a.flags & 1));
+            if (FB == 0) sym_sync<TPS>();  // staged words visible
             // map (QAMConstellationMapper.encode, constellation/models.py:240-246); the
             // 1/sqrt(N) of ifft(norm="ortho") folded in
             C x[E];
+            if constexpr (FB > 0) {
+                static_for<0, E>([&](auto I) {
+                    x[I] = active ? cscale(lut[tb.template fixed<I>()], scale) : mk<R>(0, 0);
+                });
+            } else {
+                int loff = 0;
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                const int k = t + i * TPS;
-                C v = mk<R>(0, 0);
-                if (active) {
-                    if (cm.adaptive) {
-                        const ScInfo sc = cm.sc[k];
-                        if (sc.lut >= 0) v = lut[axis[sc.lut].lut_off + extract_w(W, base_bit + sc.bitoff, sc.bits)];
-                    } else {
-                        v = lut[extract_w(W, base_bit + k * cm.b, cm.b)];
+                for (int i = 0; i < E; ++i) {
+                    const int k = t + i * TPS;
+                    C v = mk<R>(0, 0);
+                    if (active) {
+                        if (adaptive) {
+                            const ScInfo sc = cm.sc[k];
+                            if (sc.lut >= 0) {
+                                v = lut[axis[sc.lut].lut_off + tb.generic(loff, sc.bits, sc.bitoff)];
+                                loff += sc.bits;
+                            }
+                        } else {
+                            v = lut[tb.generic(loff, cm.b, k * cm.b)];
+                            loff += cm.b;
+                        }
                     }
+                    x[i] = cscale(v, scale);
                 }
-                x[i] = cscale(v, scale);
             }
             if (!(a.flags & 2)) fft_reg<R, LOGN, true>(x, row, tw, tw + 64, t);
             // PAPR statistics over the modulated symbol incl. its prefix (simulation/models.py:519-522)
@@ -161,13 +208,14 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
                 // flat channel: y = h0 x, no inter-symbol memory
                 if (active && c >= 0) {
                     R pys = 0;
+                    C* yo = yout + sl * N;
 #pragma unroll
                     for (int i = 0; i < E; ++i) {
                         const int k = t + i * TPS;
                         const C yv = cmul(h0, x[i]);
                         const R p2 = norm2(yv);
                         pys += k >= N - cp ? 2 * p2 : p2;
-                        if (yout && !(a.flags & 4)) yout[sl * N + k] = yv;
+                        if (yout && !(a.flags & 4)) yo[k] = yv;
                     }
                     py += pys;
                 }
@@ -214,18 +262,15 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
 }
 
 // ============================================================ fused RX
-// EQ: OFDM_EQ_* fixed at compile time, or -1 = read from the plan at run time.
-// FAST: fixed constellation, Philox bits and Philox (or no) noise -- the throughput
-// configuration -- with everything else compiled out; otherwise the generic kernel
-// (reference-stream bytes and normals, adaptive bit loading).
-template <typename R, int LOGN, int EQ, bool FAST>
+// EQ: OFDM_EQ_* fixed at compile time (throughput kernel) or -1 = from the plan.
+template <typename R, int LOGN, int EQ, int FB>
 __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
     using G = Geo<LOGN>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
     const TxRxCommon& cm = a.c;
     const int eq = EQ >= 0 ? EQ : cm.eq;
-    const bool adaptive = FAST ? false : (bool)cm.adaptive;
+    const bool adaptive = FB ? false : (bool)cm.adaptive;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(128);
     AxisInfo* axis = cv.take<AxisInfo>(4);
@@ -252,12 +297,12 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     R sigma = 0;
-    if (a.noise_on && !(a.flags & 1)) {
+    const bool noise = a.noise_on && !(a.flags & 1);
+    if (noise) {
         const double p = a.stats[0] / (double)a.total_samples;
         sigma = (R)sqrt((p / a.snr_lin) / 2.0);
     }
-    const bool noise = a.noise_on && !(a.flags & 1);
-    const bool array_noise = !FAST && a.nr != nullptr && noise;
+    const bool array_noise = FB == 0 && a.nr != nullptr && noise;
     const int64_t niter = (cm.n_sym + G::SPB - 1) / G::SPB;
     unsigned long long be = 0, se = 0;
 
@@ -265,8 +310,8 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
         const int64_t sl = it * G::SPB + ls;
         const int64_t sg = cm.sym0 + sl;
         const bool active = sl < cm.n_sym;
-        int base_bit = 0;
-        if (active && !(a.flags & 4)) base_bit = stage_words<TPS>(cm, sg, W, t);
+        TxBits<FB, TPS> tb;
+        tb.load(cm, sg, t, W, active && !(a.flags & 4));
         // kept channel samples + AWGN; the 1/sqrt(N) of fft(norm="ortho") folded in
         const C* ys = (const C*)a.y + sl * N;
         C x[E];
@@ -282,23 +327,20 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
                 x[i].im += sigma * (R)ni[t + i * TPS];
             }
         } else if (active && noise) {
-            // Philox noise: one call = two complex normals, for elements i and i+1
+            Xoshiro128ss g;
+            g.seed(philox_lane(cm.seed, sg, (uint32_t)t, kLaneNoise));
 #pragma unroll
-            for (int i = 0; i < E; i += 2) {
-                float r0, i0, r1, i1;
-                philox_noise_pair(cm.seed, sg, (uint32_t)(t + (i >> 1) * TPS), r0, i0, r1, i1);
-                x[i].re += sigma * (R)r0;
-                x[i].im += sigma * (R)i0;
-                if (i + 1 < E) {
-                    x[i + 1].re += sigma * (R)r1;
-                    x[i + 1].im += sigma * (R)i1;
-                }
+            for (int i = 0; i < E; ++i) {
+                float nre, nim;
+                g.normal2(nre, nim);
+                x[i].re += sigma * (R)nre;
+                x[i].im += sigma * (R)nim;
             }
         }
 #pragma unroll
         for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
         if (!(a.flags & 2)) fft_reg<R, LOGN, false>(x, row, tw, tw + 64, t);
-        sym_sync<TPS>();  // tx bit words visible to the whole symbol group
+        if (FB == 0) sym_sync<TPS>();  // staged words visible to the whole group
         // MMSE noise variance per OFDM symbol (equalization/models.py:39-49)
         R nv = 0;
         if (eq == OFDM_EQ_MMSE) {
@@ -310,10 +352,10 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
         }
         if (active && !(a.flags & 8)) {
             const int64_t sbit = sg * cm.bps;
-            const bool all_valid = FAST || sbit + cm.bps <= a.n_valid_bits;
+            const bool all_valid = FB > 0 || sbit + cm.bps <= a.n_valid_bits;
             uint32_t bes = 0, ses = 0;
-#pragma unroll
-            for (int i = 0; i < E; ++i) {
+            int loff = 0;
+            auto element = [&](int i, uint32_t tidx_fixed) {
                 const int k = t + i * TPS;
                 C v = x[i];
                 if (eq == OFDM_EQ_ZF) {
@@ -321,21 +363,30 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
                 } else if (eq == OFDM_EQ_MMSE) {
                     v = cmul(v, mmse_coef<R>(eqa[k], eqb[k], nv));
                 }
-                if (!FAST && sl < a.z_keep) ((C*)a.z_out)[sl * N + k] = v;
-                uint32_t ridx;
+                if (FB == 0 && sl < a.z_keep) ((C*)a.z_out)[sl * N + k] = v;
+                uint32_t ridx, tidx;
                 int b, off;
-                if (adaptive) {
+                if (FB > 0) {
+                    b = FB;
+                    off = k * FB;
+                    ridx = slicer(v);
+                    tidx = tidx_fixed;
+                } else if (adaptive) {
                     const ScInfo sc = cm.sc[k];
-                    if (sc.lut < 0) continue;
+                    if (sc.lut < 0) return;
                     b = sc.bits;
                     off = sc.bitoff;
                     ridx = slice<R>(v, axis[sc.lut]);
+                    tidx = tb.generic(loff, b, off);
+                    loff += b;
                 } else {
                     b = cm.b;
                     off = k * b;
                     ridx = slicer(v);
+                    tidx = tb.generic(loff, b, off);
+                    loff += b;
                 }
-                uint32_t d = ridx ^ extract_w(W, base_bit + off, b);
+                uint32_t d = ridx ^ tidx;
                 ses += d != 0u;
                 if (!all_valid) {
                     const int64_t nvb = a.n_valid_bits - (sbit + off);
@@ -343,6 +394,12 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
                     d &= ((1u << keep) - 1u) << (b - keep);
                 }
                 bes += __popc(d);
+            };
+            if constexpr (FB > 0) {
+                static_for<0, E>([&](auto I) { element(I, tb.template fixed<I>()); });
+            } else {
+#pragma unroll
+                for (int i = 0; i < E; ++i) element(i, 0u);
             }
             be += bes;
             se += ses;

@@ -22,6 +22,8 @@ static hipError_t set_smem(F fn, size_t bytes) {
     return e;
 }
 
+constexpr int kFastMinLogN = 6;  // throughput specialisations for N >= 64
+
 static inline int clamp_grid(int64_t want) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, kMaxGrid));
 }
@@ -99,14 +101,32 @@ hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <typename R, int LOGN>
-static hipError_t tx_one(const TxArgs& a, int grid, hipStream_t s) {
+template <typename R, int LOGN, int FB>
+static hipError_t tx_launch(const TxArgs& a, int grid, hipStream_t s) {
     const size_t sm = smem_tx<R>(LOGN, a.c.lut_len, a.c.words_per_sym, a.L, a.c.cp);
-    auto fn = k_tx<R, LOGN>;
+    auto fn = k_tx<R, LOGN, FB>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), sm, s, a);
     return hipGetLastError();
+}
+
+// Throughput configuration (complex64, fixed square QAM, Philox bits; N >= 64) -> the
+// kernel specialised on the bits per subcarrier; anything else -> the generic kernel.
+template <typename R, int LOGN>
+static hipError_t tx_one(const TxArgs& a, int grid, hipStream_t s) {
+    if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
+        if (!a.c.adaptive && a.c.bits == nullptr) {
+            switch (a.c.b) {
+                case 2: return tx_launch<R, LOGN, 2>(a, grid, s);
+                case 4: return tx_launch<R, LOGN, 4>(a, grid, s);
+                case 6: return tx_launch<R, LOGN, 6>(a, grid, s);
+                case 8: return tx_launch<R, LOGN, 8>(a, grid, s);
+                default: break;
+            }
+        }
+    }
+    return tx_launch<R, LOGN, 0>(a, grid, s);
 }
 
 template <typename R>
@@ -122,28 +142,40 @@ hipError_t launch_tx(int logn, const TxArgs& a, int grid, hipStream_t s) {
 #undef OFDM_TX_CASE
 }
 
-template <typename R, int LOGN, int EQ, bool FAST>
+template <typename R, int LOGN, int EQ, int FB>
 static hipError_t rx_launch(const RxArgs& a, int grid, hipStream_t s) {
     const size_t sm = smem_rx<R>(LOGN, a.c.words_per_sym);
-    auto fn = k_rx<R, LOGN, EQ, FAST>;
+    auto fn = k_rx<R, LOGN, EQ, FB>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), sm, s, a);
     return hipGetLastError();
 }
 
-// Throughput configuration (complex64, fixed QAM, Philox bits + noise) -> specialised
-// kernel with the equaliser compiled in; anything else -> the generic kernel.
+template <typename R, int LOGN, int FB>
+static hipError_t rx_eq(const RxArgs& a, int grid, hipStream_t s) {
+    if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, FB>(a, grid, s);
+    if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, FB>(a, grid, s);
+    return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB>(a, grid, s);
+}
+
+// Throughput configuration (complex64, fixed square QAM, Philox bits and noise, no
+// received-symbol tap; N >= 64) -> kernel specialised on bits and equaliser; anything
+// else -> the generic kernel.
 template <typename R, int LOGN>
 static hipError_t rx_one(const RxArgs& a, int grid, hipStream_t s) {
-    const bool fast = sizeof(R) == 4 && !a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr &&
-                      a.z_out == nullptr;
-    if (fast) {
-        if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, true>(a, grid, s);
-        if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, true>(a, grid, s);
-        return rx_launch<R, LOGN, OFDM_EQ_MMSE, true>(a, grid, s);
+    if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
+        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr) {
+            switch (a.c.b) {
+                case 2: return rx_eq<R, LOGN, 2>(a, grid, s);
+                case 4: return rx_eq<R, LOGN, 4>(a, grid, s);
+                case 6: return rx_eq<R, LOGN, 6>(a, grid, s);
+                case 8: return rx_eq<R, LOGN, 8>(a, grid, s);
+                default: break;
+            }
+        }
     }
-    return rx_launch<R, LOGN, -1, false>(a, grid, s);
+    return rx_launch<R, LOGN, -1, 0>(a, grid, s);
 }
 
 template <typename R>
