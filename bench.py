@@ -152,9 +152,11 @@ def main():
     events = []
     bit_errors = 0
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        st = engine.run(total, snr, seed=k, group=group, events=events)
-        bit_errors += st.bit_errors
+    # every step is the whole hot path (bits -> ... -> error counts); the host enqueues
+    # step k+1 while the GPU runs step k and reads all counts back inside the timed region
+    pending = [engine.run_async(total, snr, seed=k, group=group, events=events) for k in range(args.steps)]
+    for p in pending:
+        bit_errors += p.result().bit_errors
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

@@ -94,7 +94,7 @@ struct ofdm_plan_s {
     int n, logn, cp, prec, eq, L;
     int adaptive, b, bps, n_axis, lut_len, n_active;
     double gain_mean;
-    DevBuf tw, lut, lut64, h, eq_a, eq_b, axis, sc, active, ws, H64;
+    DevBuf tw, ptw, lut, lut64, h, eq_a, eq_b, axis, sc, active, ws, H64;
     int has_const, has_channel, separable, zp;
     size_t csize() const { return prec == OFDM_F32 ? 8 : 16; }
 };
@@ -232,6 +232,30 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
             tw[2 * (64 + j) + 1] = std::sin(a2);
         }
         if ((rc = upload_cpx(p->tw, tw, p->prec, s))) return rc;
+    }
+    // per-pass twiddle tables of the throughput kernels (ofdm_device.hpp tt_from):
+    // [forward | inverse], pass (LOGR, LOGNS > 0): T[(r-1) NS + k] = exp(-+2 pi i k r / (NS RAD))
+    if (p->logn > 4) {
+        const int tts = tt_size(p->logn);
+        std::vector<double> tt(4 * (size_t)tts, 0.0);
+        size_t at = 0;
+        for (int logns = 0; logns < p->logn;) {
+            const int logr = std::min(4, p->logn - logns);
+            const int ns = 1 << logns, rad = 1 << logr;
+            if (logns > 0) {
+                for (int r = 1; r < rad; ++r)
+                    for (int k = 0; k < ns; ++k, ++at) {
+                        const double a = -2.0 * M_PI * (double)(k * r) / (double)(ns * rad);
+                        tt[2 * at] = std::cos(a);
+                        tt[2 * at + 1] = std::sin(a);
+                        tt[2 * (tts + at)] = std::cos(a);
+                        tt[2 * (tts + at) + 1] = -std::sin(a);
+                    }
+            }
+            logns += logr;
+        }
+        if ((int)at != tts) return fail(OFDM_E_INVALID, "internal: twiddle table size");
+        if ((rc = upload_cpx(p->ptw, tt, p->prec, s))) return rc;
     }
 
     // constellations
@@ -554,6 +578,7 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
     c.sym0 = sym0;
     c.n_sym = n_sym;
     c.tw = p->tw.p;
+    c.ptw = p->ptw.p;
     c.lut = p->lut.p;
     c.lut_len = p->lut_len;
     c.axis = (const AxisInfo*)p->axis.p;
@@ -589,11 +614,8 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
     a.chunk = p->L > 1 ? 16 : 1;
     a.slot = tx_slot(p->logn, p->cp, p->L);
     a.flags = env_flags("OFDM_ABLATE_TX");
-    const int spb = geo_spb(p->logn);
-    const int64_t groups = (n_sym + a.chunk - 1) / a.chunk;
-    const int64_t iters = (groups + spb - 1) / spb;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(iters, kMaxGrid));
-#define CALL(R) launch_tx<R>(p->logn, a, grid, (hipStream_t)stream)
+    int grid = 0;  // chosen by the launcher with the kernel (<= kMaxGrid partial records)
+#define CALL(R) launch_tx<R>(p->logn, a, &grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));
 #undef CALL
     return reduce_into(p, (hipStream_t)stream, grid, 3, 4, stats);
@@ -625,10 +647,8 @@ int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const 
     a.z_out = z_out;
     a.z_keep = z_out ? z_keep : 0;
     a.flags = env_flags("OFDM_ABLATE_RX");
-    const int spb = geo_spb(p->logn);
-    const int64_t iters = (n_sym + spb - 1) / spb;
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(iters, kMaxGrid));
-#define CALL(R) launch_rx<R>(p->logn, a, grid, (hipStream_t)stream)
+    int grid = 0;
+#define CALL(R) launch_rx<R>(p->logn, a, &grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));
 #undef CALL
     return OFDM_OK;

@@ -53,6 +53,56 @@ __device__ __forceinline__ cpx<R> rot90(cpx<R> a) {
 template <typename R>
 __device__ __forceinline__ R norm2(cpx<R> a) { return a.re * a.re + a.im * a.im; }
 
+// complex64 on the packed-f32 VALU: v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 do both
+// components in one issue slot (the f32 vector peak of CDNA4 is only reached packed);
+// swizzles and negations fold into the op_sel / neg_lo / neg_hi operand modifiers.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <>
+struct cpx<float> {
+    union {
+        f32x2 v;
+        struct {
+            float re, im;
+        };
+    };
+};
+__device__ __forceinline__ cpx<float> pk(f32x2 v) {
+    cpx<float> c;
+    c.v = v;
+    return c;
+}
+template <>
+__device__ __forceinline__ cpx<float> mk<float>(float a, float b) { return pk(f32x2{a, b}); }
+template <>
+__device__ __forceinline__ cpx<float> operator+<float>(cpx<float> a, cpx<float> b) { return pk(a.v + b.v); }
+template <>
+__device__ __forceinline__ cpx<float> operator-<float>(cpx<float> a, cpx<float> b) { return pk(a.v - b.v); }
+template <>
+__device__ __forceinline__ cpx<float> cmul<float>(cpx<float> a, cpx<float> b) {
+    // (ar br, ar bi) + (ai, ai) * (-bi, br): the swizzle and negation of b fold into
+    // op_sel / neg_lo when b has one use, so pass the twiddle as a (splatted) and the data as b
+    return pk(__builtin_elementwise_fma(a.v.yy, f32x2{-b.v.y, b.v.x}, a.v.xx * b.v));
+}
+template <>
+__device__ __forceinline__ cpx<float> cscale<float>(cpx<float> a, float s) { return pk(a.v * s); }
+
+// a * b for two run-time values: 2 packed instructions.  The compiler materialises the
+// swizzled, negated b with a v_xor + v_mov pair whenever b has another use, so the fma
+// is spelt out: lo = a.y * -b.y + t.x, hi = a.y * b.x + t.y.
+template <typename R>
+__device__ __forceinline__ cpx<R> cmulv(cpx<R> a, cpx<R> b) {
+    if constexpr (sizeof(R) == 4) {
+        const f32x2 t = a.v.xx * b.v;
+        f32x2 r;
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+            : "=v"(r)
+            : "v"(a.v), "v"(b.v), "v"(t));
+        return pk(r);
+    } else {
+        return cmul(a, b);
+    }
+}
+
 // ------------------------------------------------------------------ small DFTs
 template <typename R, bool INV>
 __device__ __forceinline__ void dft2(cpx<R>& a, cpx<R>& b) {
@@ -61,13 +111,35 @@ __device__ __forceinline__ void dft2(cpx<R>& a, cpx<R>& b) {
     b = t;
 }
 
-template <typename R, bool INV>
+// a + rot90(d) (SGN = +1) or a - rot90(d) (SGN = -1).  complex64: one v_pk_fma_f32 on
+// the swizzled operand, so the rotation is never materialised.
+template <typename R, bool INV, int SGN>
+__device__ __forceinline__ cpx<R> add_rot(cpx<R> a, cpx<R> d) {
+    if constexpr (sizeof(R) == 4) {
+        constexpr float s = (INV ? -1.f : 1.f) * SGN;
+        return pk(__builtin_elementwise_fma(d.v.yx, f32x2{s, -s}, a.v));
+    } else {
+        const cpx<R> r = rot90<R, INV>(d);
+        return SGN > 0 ? a + r : a - r;
+    }
+}
+
+// ROT2: v2 enters multiplied by -i (forward) / +i (inverse)
+template <typename R, bool INV, bool ROT2 = false>
 __device__ __forceinline__ void dft4(cpx<R>& v0, cpx<R>& v1, cpx<R>& v2, cpx<R>& v3) {
-    cpx<R> t0 = v0 + v2, t1 = v0 - v2, t2 = v1 + v3, t3 = rot90<R, INV>(v1 - v3);
+    cpx<R> t0, t1;
+    if constexpr (ROT2) {
+        t0 = add_rot<R, INV, 1>(v0, v2);
+        t1 = add_rot<R, INV, -1>(v0, v2);
+    } else {
+        t0 = v0 + v2;
+        t1 = v0 - v2;
+    }
+    const cpx<R> t2 = v1 + v3, d = v1 - v3;
     v0 = t0 + t2;
     v2 = t0 - t2;
-    v1 = t1 + t3;
-    v3 = t1 - t3;
+    v1 = add_rot<R, INV, 1>(t1, d);
+    v3 = add_rot<R, INV, -1>(t1, d);
 }
 
 // W_n^k = exp(-+2 pi i k / n), compile-time constants for n = 8, 16
@@ -116,13 +188,17 @@ __device__ __forceinline__ void dft(cpx<R>* v) {
             dft4<R, INV>(a[n2][0], a[n2][1], a[n2][2], a[n2][3]);
         }
         a[1][1] = cmul(a[1][1], w16<R, INV>(2));
-        a[1][2] = rot90<R, INV>(a[1][2]);
         a[1][3] = cmul(a[1][3], w16<R, INV>(6));
 #pragma unroll
         for (int k1 = 0; k1 < 4; ++k1) {
             cpx<R> p = a[0][k1], q = a[1][k1];
-            v[k1] = p + q;
-            v[k1 + 4] = p - q;
+            if (k1 == 2) {  // q * W8^2 = rot90(q)
+                v[k1] = add_rot<R, INV, 1>(p, q);
+                v[k1 + 4] = add_rot<R, INV, -1>(p, q);
+            } else {
+                v[k1] = p + q;
+                v[k1 + 4] = p - q;
+            }
         }
     } else if constexpr (RAD == 16) {
         // n = 4 n1 + n2, k = k1 + 4 k2
@@ -140,15 +216,15 @@ __device__ __forceinline__ void dft(cpx<R>* v) {
 #pragma unroll
             for (int k1 = 1; k1 < 4; ++k1) {
                 const int e = n2 * k1;
-                if (e == 4)
-                    a[n2][k1] = rot90<R, INV>(a[n2][k1]);
-                else
-                    a[n2][k1] = cmul(a[n2][k1], w16<R, INV>(e));
+                if (e != 4) a[n2][k1] = cmul(a[n2][k1], w16<R, INV>(e));  // e = 4: ROT2 below
             }
 #pragma unroll
         for (int k1 = 0; k1 < 4; ++k1) {
             cpx<R> b0 = a[0][k1], b1 = a[1][k1], b2 = a[2][k1], b3 = a[3][k1];
-            dft4<R, INV>(b0, b1, b2, b3);
+            if (k1 == 2)
+                dft4<R, INV, true>(b0, b1, b2, b3);
+            else
+                dft4<R, INV>(b0, b1, b2, b3);
             v[k1] = b0;
             v[k1 + 4] = b1;
             v[k1 + 8] = b2;
@@ -158,17 +234,29 @@ __device__ __forceinline__ void dft(cpx<R>* v) {
 }
 
 // ------------------------------------------------------------------ FFT geometry
-template <int LOGN>
+template <int LOGN, int BLK = kBlock>
 struct Geo {
     static constexpr int N = 1 << LOGN;
     static constexpr int LOGE = LOGN < 4 ? LOGN : 4;
     static constexpr int E = 1 << LOGE;   // elements per thread
     static constexpr int TPS = N / E;     // threads per symbol
-    static constexpr int SPB = kBlock / TPS;  // symbols per workgroup
-    static constexpr int PADN = N + (N >> 4) + 1;  // padded LDS row (complex elements)
+    static constexpr int SPB = BLK / TPS;  // symbols per workgroup
+    static constexpr int PADN = N + (N >> 4);  // padded LDS row (complex elements); with pad()
+                                                // conflict-free row spacing (tools/lds_banks.py)
 };
 
 __device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
+
+// Per-pass twiddle tables (throughput kernels).  Pass (LOGR, LOGNS > 0) multiplies input r
+// of butterfly k = j mod NS by W^(k r), W = exp(-+2 pi i / (NS RAD)); the tables hold
+// T[(r - 1) NS + k] for 0 < r < RAD, k < NS, pass after pass, computed on the host in
+// double.  One LDS read per twiddle instead of the two-level lookup and the recurrence.
+constexpr int tt_from(int logn, int logns) {
+    if (logns >= logn) return 0;
+    const int logr = logn - logns >= 4 ? 4 : logn - logns;
+    return (logns > 0 ? ((1 << logr) - 1) << logns : 0) + tt_from(logn, logns + logr);
+}
+constexpr int tt_size(int logn) { return logn <= 4 ? 0 : tt_from(logn, 0); }
 
 // Twiddle W_N^m = exp(-2 pi i m / N) (conjugated for the inverse) from a two-level
 // table held in LDS: lo[m & 63] * hi[m >> 6].  Both tables are computed on the host
@@ -284,9 +372,9 @@ __device__ __forceinline__ void sym_sync() {
 // FIRST: inputs come from x[] (valid because the first pass has RAD = E, STRIDE = TPS);
 // LAST: outputs stay in x[] (the last pass writes j + r*NS with j = t + q*TPS and
 // NS = TPS*E/RAD, i.e. element t + (q + r*NB)*TPS); otherwise through the LDS row.
-template <typename R, int LOGN, int LOGR, int LOGNS, bool INV, bool FIRST, bool LAST>
+template <typename R, int LOGN, int LOGR, int LOGNS, bool INV, bool FIRST, bool LAST, bool TT>
 __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, const cpx<R>* lo,
-                                         const cpx<R>* hi, int t) {
+                                         const cpx<R>* hi, const cpx<R>* tt, int t) {
     using G = Geo<LOGN>;
     constexpr int RAD = 1 << LOGR;
     constexpr int NS = 1 << LOGNS;
@@ -308,15 +396,19 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
     for (int q = 0; q < NB; ++q) {
         const int j = t + q * G::TPS;
         const int k = j & (NS - 1);
-        if constexpr (LOGNS > 0) {
+        if constexpr (LOGNS > 0 && TT) {
+            const cpx<R>* T = tt + (tt_size(LOGN) - tt_from(LOGN, LOGNS)) + k;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) v[q][r] = cmulv(T[(r - 1) * NS], v[q][r]);
+        } else if constexpr (LOGNS > 0) {
             // w^r by recurrence from one table lookup: 2 live registers instead of the
             // RAD-1 hoisted table loads (<= 15 roundings: ~1e-6 in f32, ~2e-15 in f64)
             const cpx<R> w1 = twiddle<R, LOGN, INV>(k << (LOGN - LOGNS - LOGR), lo, hi);
             cpx<R> wr = w1;
 #pragma unroll
             for (int r = 1; r < RAD; ++r) {
-                v[q][r] = cmul(v[q][r], wr);
-                if (r + 1 < RAD) wr = cmul(wr, w1);
+                v[q][r] = cmulv(wr, v[q][r]);
+                if (r + 1 < RAD) wr = cmulv(wr, w1);
             }
         }
         dft<R, RAD, INV>(v[q]);
@@ -332,27 +424,28 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
     if constexpr (!LAST) sym_sync<G::TPS>();
 }
 
-template <typename R, int LOGN, int LOGNS, bool INV>
+template <typename R, int LOGN, int LOGNS, bool INV, bool TT>
 __device__ __forceinline__ void reg_passes(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, const cpx<R>* lo,
-                                           const cpx<R>* hi, int t) {
+                                           const cpx<R>* hi, const cpx<R>* tt, int t) {
     if constexpr (LOGNS < LOGN) {
         constexpr int REM = LOGN - LOGNS;
         constexpr int LOGR = REM >= 4 ? 4 : REM;
-        reg_pass<R, LOGN, LOGR, LOGNS, INV, LOGNS == 0, LOGNS + LOGR == LOGN>(x, buf, lo, hi, t);
-        reg_passes<R, LOGN, LOGNS + LOGR, INV>(x, buf, lo, hi, t);
+        reg_pass<R, LOGN, LOGR, LOGNS, INV, LOGNS == 0, LOGNS + LOGR == LOGN, TT>(x, buf, lo, hi, tt, t);
+        reg_passes<R, LOGN, LOGNS + LOGR, INV, TT>(x, buf, lo, hi, tt, t);
     }
 }
 
 // FFT of one symbol: on entry and exit thread t (of TPS) holds element t + i*TPS in
 // x[i].  Unnormalised.  buf is the symbol's private padded LDS row; the caller must
-// sym_sync() between an earlier use of buf and this call when TPS > 64.
-template <typename R, int LOGN, bool INV>
+// sym_sync() between an earlier use of buf and this call when TPS > 64.  Twiddles from the
+// two-level table lo/hi (recurrence) or, TT, from the per-pass tables tt in LDS.
+template <typename R, int LOGN, bool INV, bool TT = false>
 __device__ __forceinline__ void fft_reg(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, const cpx<R>* lo,
-                                        const cpx<R>* hi, int t) {
+                                        const cpx<R>* hi, int t, const cpx<R>* tt = nullptr) {
     if constexpr (LOGN <= 4) {
         dft<R, (1 << LOGN), INV>(x);  // one register-resident pass (TPS = 1)
     } else {
-        reg_passes<R, LOGN, 0, INV>(x, buf, lo, hi, t);
+        reg_passes<R, LOGN, 0, INV, TT>(x, buf, lo, hi, tt, t);
     }
 }
 
@@ -392,11 +485,83 @@ struct Slicer {
     }
 };
 
+// Throughput-mode slicer (complex64, square QAM with b = FB <= 8 bits).  Both axes per
+// packed op: y = z * inv_step - lev0 * inv_step (the level coordinate, offset (side-1)/2
+// is a half-integer so it must be added before rounding), then y + 1.5*2^23 leaves
+// round(y) in the low mantissa bits (round-to-nearest-even; a tie is a decision boundary,
+// probability zero under noise), clamped to [0, side-1] on the raw bits by v_med3_i32.  The levels of
+// four elements are gathered into one selector word (byte j = element j) and looked up
+// with v_perm_b32 in byte tables: four rx indices per instruction, byte-aligned like the
+// lane's tx bits (lane_bits).
+template <int FB>
+struct PermSlicer {
+    static constexpr int SIDE = 1 << (FB / 2), HB = FB / 2;
+    static constexpr int MAGIC = 0x4B400000;  // bit pattern of 1.5 * 2^23
+    static constexpr uint32_t BYTE_MASK = 0x01010101u * ((1u << FB) - 1u);
+    f32x2 mul, add, magic;
+    uint32_t ti[4], tq[4];  // byte k: ipat[k] / qpat[k] << HB (k < SIDE)
+
+    // scale: factor between the slicer input and the constellation's scale (1/sqrt(N)
+    // when the FFT output is left unnormalised)
+    __device__ void load(const AxisInfo& a, float scale) {
+        const float is = (float)(a.inv_step * (double)scale);
+        const float off = (float)(-a.lev0 * a.inv_step);
+        mul = f32x2{is, is};
+        add = f32x2{off, off};
+        magic = f32x2{12582912.0f, 12582912.0f};
+        for (int w = 0; w < 4; ++w) ti[w] = tq[w] = 0u;
+        for (int k = 0; k < SIDE; ++k) {
+            ti[k >> 2] |= (uint32_t)a.ipat[k] << (8 * (k & 3));
+            tq[k >> 2] |= ((uint32_t)a.qpat[k] << HB) << (8 * (k & 3));
+        }
+    }
+    __device__ __forceinline__ static uint32_t clampl(float f) {
+        const int u = __builtin_bit_cast(int, f);
+        return (uint32_t)min(max(u, MAGIC), MAGIC + SIDE - 1);  // level in the low byte
+    }
+    // byte j of the result = table[byte j of sel]
+    __device__ __forceinline__ static uint32_t lookup(const uint32_t (&tb)[4], uint32_t sel) {
+        if constexpr (SIDE <= 8) {
+            return __builtin_amdgcn_perm(tb[1], tb[0], sel);
+        } else {
+            const uint32_t s7 = sel & 0x07070707u;
+            const uint32_t lo = __builtin_amdgcn_perm(tb[1], tb[0], s7);
+            const uint32_t hi = __builtin_amdgcn_perm(tb[3], tb[2], s7);
+            // 0xff in byte j when bit 3 of byte j of sel is set: the perm sign selectors
+            // 8..11 read bit 7 of bytes 1, 3 (S1) and 5, 7 (S0)
+            const uint32_t m = __builtin_amdgcn_perm(sel << 12, sel << 4, 0x090B080Au);
+            return (hi & m) | (lo & ~m);
+        }
+    }
+    // (rx ^ tx) indices of four elements, one per byte; txw = the lane word (unmasked)
+    __device__ __forceinline__ uint32_t diff(const cpx<float> (&z)[4], uint32_t txw) const {
+        uint32_t li[4], lq[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x2 f = __builtin_elementwise_fma(z[j].v, mul, add) + magic;
+            li[j] = clampl(f.x);
+            lq[j] = clampl(f.y);
+        }
+        const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
+                                                  __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
+        const uint32_t sq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(lq[3], lq[2], 0x0c0c0400u),
+                                                  __builtin_amdgcn_perm(lq[1], lq[0], 0x0c0c0400u), 0x05040100u);
+        return (lookup(ti, si) | lookup(tq, sq)) ^ (txw & BYTE_MASK);
+    }
+    // number of non-zero bytes
+    __device__ __forceinline__ static uint32_t nonzero_bytes(uint32_t d) {
+        if constexpr (FB < 8)
+            return __popc((d + 0x7F7F7F7Fu) & 0x80808080u);  // bytes < 0x80: no carry out
+        else
+            return __popc((((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u);
+    }
+};
+
 // ------------------------------------------------------------------ reductions
 // Sum over the TPS threads of one symbol group (t = threadIdx.x % TPS).  All threads
 // of the workgroup must call it (uses a workgroup barrier for TPS > 64).
 template <typename T, int TPS>
-__device__ __forceinline__ T group_sum(T v, T* scratch /* kBlock entries */) {
+__device__ __forceinline__ T group_sum(T v, T* scratch /* block / 64 entries */) {
     if constexpr (TPS == 1) {
         return v;
     } else if constexpr (TPS <= 64) {
@@ -419,21 +584,21 @@ __device__ __forceinline__ T group_sum(T v, T* scratch /* kBlock entries */) {
     }
 }
 
-template <typename T>
-__device__ __forceinline__ T block_sum(T v, T* scratch) {
+template <typename T, int BLK = kBlock>
+__device__ __forceinline__ T block_sum(T v, T* scratch /* BLK / 64 entries */) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
     __syncthreads();
     T s = 0;
     if (threadIdx.x == 0)
-        for (int w = 0; w < kBlock / 64; ++w) s += scratch[w];
+        for (int w = 0; w < BLK / 64; ++w) s += scratch[w];
     __syncthreads();
     return s;  // valid in thread 0
 }
 
-template <typename T>
-__device__ __forceinline__ T block_max(T v, T* scratch) {
+template <typename T, int BLK = kBlock>
+__device__ __forceinline__ T block_max(T v, T* scratch /* BLK / 64 entries */) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         T o = __shfl_xor(v, off, 64);
@@ -443,7 +608,7 @@ __device__ __forceinline__ T block_max(T v, T* scratch) {
     __syncthreads();
     T s = 0;
     if (threadIdx.x == 0)
-        for (int w = 0; w < kBlock / 64; ++w) s = scratch[w] > s ? scratch[w] : s;
+        for (int w = 0; w < BLK / 64; ++w) s = scratch[w] > s ? scratch[w] : s;
     __syncthreads();
     return s;
 }
@@ -454,15 +619,18 @@ struct u4 {
 };
 
 __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
+    // keep the key schedule in the loop (SALU adds next to the VALU rounds): hoisted out of
+    // a symbol loop it is 20 live SGPRs and spills
+    asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        // one v_mad_u64_u32 per 32x32->64 product
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
         u4 n;
-        n.x = hi1 ^ c.y ^ k0;
-        n.y = lo1;
-        n.z = hi0 ^ c.w ^ k1;
-        n.w = lo0;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
         c = n;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -470,51 +638,14 @@ __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-constexpr uint32_t kStreamBits = 0xB175B175u;
-constexpr uint32_t kStreamNoise = 0x4015E000u;
-
-// Philox bit word w of OFDM symbol s: word (w & 3) of block (w >> 2).
-__device__ __forceinline__ u4 philox_bits_block(uint64_t seed, int64_t s, uint32_t blk) {
-    u4 c;
-    c.x = blk;
-    c.y = (uint32_t)s;
-    c.z = (uint32_t)((uint64_t)s >> 32);
-    c.w = kStreamBits;
-    return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-}
-
-// Two standard complex normals (re, im each N(0,1)) for kept samples 2p, 2p+1 of
-// symbol s.  Box-Muller in fp32 on the hardware transcendentals: v_log_f32 (log2),
-// v_sqrt_f32, v_sin_f32 / v_cos_f32 (argument in revolutions).
-__device__ __forceinline__ void philox_noise_pair(uint64_t seed, int64_t s, uint32_t p, float& r0,
-                                                  float& i0, float& r1, float& i1) {
-    u4 c;
-    c.x = p;
-    c.y = (uint32_t)s;
-    c.z = (uint32_t)((uint64_t)s >> 32);
-    c.w = kStreamNoise;
-    const u4 o = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-    const float k = 2.3283064365386963e-10f;  // 2^-32
-    const float u0 = ((float)o.x + 0.5f) * k, v0 = ((float)o.y) * k;
-    const float u1 = ((float)o.z + 0.5f) * k, v1 = ((float)o.w) * k;
-    const float a0 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u0));
-    const float a1 = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u1));
-    r0 = a0 * __builtin_amdgcn_cosf(v0);
-    i0 = a0 * __builtin_amdgcn_sinf(v0);
-    r1 = a1 * __builtin_amdgcn_cosf(v1);
-    i1 = a1 * __builtin_amdgcn_sinf(v1);
-}
-
 // ------------------------------------------------------------------ throughput-mode streams
-// Definition (philox mode): thread t of OFDM symbol s owns elements k = t + TPS*i.
-//  * bits : one Philox4x32-10 block keyed (seed; ctr = t, s, kLaneBits) = 128 bits,
-//           MSB-first; element i takes the next b_k bits in element order.
-//  * noise: xoshiro128** seeded by one Philox4x32-10 block (seed; t, s, kLaneNoise);
-//           element i consumes two outputs (u1, u2) -> Box-Muller -> (re, im).
-// Both depend only on (seed, s, N), so results do not depend on how symbols are
-// batched or sharded across GPUs.
-constexpr uint32_t kLaneBits = 0x1A7EB175u;
-constexpr uint32_t kLaneNoise = 0x1A7E4015u;
+// Definition (philox mode): thread t of OFDM symbol s owns elements k = t + TPS*i.  Its
+// lane generator is SFC32 seeded with words 0..2 of one Philox4x32-10 block, key = seed,
+// counter = (t, s mod 2^32, s >> 32, kLane).  Outputs 0..3 are the lane's 128 payload
+// bits (element i takes the low b_k bits of byte i, see lane_bits); outputs 4+3j, 5+3j,
+// 6+3j give the complex noise of elements 2j, 2j+1 (Sfc32::add_noise2).  Everything depends only on
+// (seed, s, N), so results do not depend on how symbols are batched or sharded.
+constexpr uint32_t kLane = 0x1A7E5EEDu;
 
 __device__ __forceinline__ u4 philox_lane(uint64_t seed, int64_t s, uint32_t t, uint32_t stream) {
     u4 c;
@@ -525,57 +656,47 @@ __device__ __forceinline__ u4 philox_lane(uint64_t seed, int64_t s, uint32_t t, 
     return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
 }
 
-// b bits at compile-time offset O of the 128-bit block w0..w3.
-template <int O, int Bb>
-__device__ __forceinline__ uint32_t bits128_c(const u4& w) {
-    constexpr int q = O >> 5, s = O & 31;
-    const uint32_t a[4] = {w.x, w.y, w.z, w.w};
-    if constexpr (s + Bb <= 32) {
-        return (a[q] >> (32 - s - Bb)) & ((1u << Bb) - 1u);
-    } else {
-        return ((a[q] << (s + Bb - 32)) | (a[q + 1] >> (64 - s - Bb))) & ((1u << Bb) - 1u);
-    }
+// Element i of a lane takes the low b bits of byte i of the lane's 128-bit block
+// (byte i = bits 8*(i&3).. of word i>>2): one v_bfe_u32, and four elements of the rx
+// decisions compare against one word.
+__device__ __forceinline__ uint32_t lane_word(const u4& w, int q) {
+    return q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+}
+__device__ __forceinline__ uint32_t lane_bits(const u4& w, int i, int b) {
+    return (lane_word(w, i >> 2) >> (8 * (i & 3))) & ((1u << b) - 1u);
 }
 
-// b bits at run-time offset o (o + b <= 128).
-__device__ __forceinline__ uint32_t bits128(const u4& w, int o, int b) {
-    const int q = o >> 5, s = o & 31;
-    const uint32_t hi = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
-    const uint32_t lo = q == 0 ? w.y : q == 1 ? w.z : q == 2 ? w.w : 0u;
-    const uint64_t x = ((uint64_t)hi << 32) | lo;
-    return (uint32_t)(x >> (64 - s - b)) & ((1u << b) - 1u);
-}
-
-// xoshiro128** (Blackman & Vigna): 4x32-bit state, ~12 simple ALU ops per output.
-struct Xoshiro128ss {
-    uint32_t s0, s1, s2, s3;
-    __device__ __forceinline__ static uint32_t rotl(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+// SFC32 (Doty-Humphrey's small fast counting generator): 96-bit state plus a counter,
+// 6 ALU ops per output.  The counter is the draw index, a compile-time constant in the
+// unrolled lane loops, so it costs nothing; the state comes from a Philox block.
+struct Sfc32 {
+    uint32_t a, b, c, n;
     __device__ __forceinline__ void seed(const u4& v) {
-        s0 = v.x;
-        s1 = v.y;
-        s2 = v.z;
-        s3 = v.w | ((v.x | v.y | v.z) == 0u ? 1u : 0u);  // never the all-zero state
+        a = v.x;
+        b = v.y;
+        c = v.z;
+        n = 0u;
     }
     __device__ __forceinline__ uint32_t next() {
-        const uint32_t r = rotl(s1 * 5u, 7) * 9u;
-        const uint32_t t = s1 << 9;
-        s2 ^= s0;
-        s3 ^= s1;
-        s1 ^= s2;
-        s0 ^= s3;
-        s2 ^= t;
-        s3 = rotl(s3, 11);
+        const uint32_t r = a + b + (++n);
+        a = b ^ (b >> 9);
+        b = c + (c << 3);
+        c = ((c << 21) | (c >> 11)) + r;
         return r;
     }
-    // one complex standard normal (re, im each N(0,1)) by Box-Muller on the hardware
-    // transcendentals (v_log_f32 = log2, v_sin/cos_f32 take revolutions)
-    __device__ __forceinline__ void normal2(float& re, float& im) {
-        const float k = 2.3283064365386963e-10f;  // 2^-32
-        const float u = ((float)next() + 0.5f) * k;
-        const float v = (float)next() * k;
-        const float a = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u));
-        re = a * __builtin_amdgcn_cosf(v);
-        im = a * __builtin_amdgcn_sinf(v);
+    // Two complex normals with per-component standard deviation sigma added to x0, x1, by
+    // Box-Muller on the hardware transcendentals (v_log_f32 = log2, v_sin/cos_f32 take
+    // revolutions): three outputs -- radius words u0, u1 (32 bits each, so the Rayleigh
+    // tail is exact to 6.7 sigma) and one angle word whose high / low 16 bits are the two
+    // phases.  x += sigma sqrt(-2 ln u) (cos 2 pi v, sin 2 pi v), u in (0, 1], v in [0, 1).
+    __device__ __forceinline__ void add_noise2(f32x2& x0, f32x2& x1, float m2s2ln2 /* -2 ln2 sigma^2 */) {
+        const float k32 = 2.3283064365386963e-10f, k16 = 1.52587890625e-05f;  // 2^-32, 2^-16
+        const uint32_t w0 = next(), w1 = next(), wa = next();
+        const float r0 = __builtin_amdgcn_sqrtf(m2s2ln2 * __builtin_amdgcn_logf(((float)w0 + 0.5f) * k32));
+        const float r1 = __builtin_amdgcn_sqrtf(m2s2ln2 * __builtin_amdgcn_logf(((float)w1 + 0.5f) * k32));
+        const float v0 = (float)(wa >> 16) * k16, v1 = (float)(wa & 0xFFFFu) * k16;
+        x0 = __builtin_elementwise_fma(f32x2{__builtin_amdgcn_cosf(v0), __builtin_amdgcn_sinf(v0)}, f32x2{r0, r0}, x0);
+        x1 = __builtin_elementwise_fma(f32x2{__builtin_amdgcn_cosf(v1), __builtin_amdgcn_sinf(v1)}, f32x2{r1, r1}, x1);
     }
 };
 

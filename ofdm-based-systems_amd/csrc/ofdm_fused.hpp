@@ -26,8 +26,23 @@
 #ifndef OFDM_RX_WAVES
 #define OFDM_RX_WAVES 1
 #endif
+// Workgroup of the throughput (FB > 0) kernels at N <= 1024 (TX; RX without equaliser):
+// 8 waves share one copy of the twiddle tables and two workgroups fit the 160 KB LDS, i.e.
+// 4 waves per SIMD (register budget 128).  Other variants: 256 threads, OFDM_*_WAVES.
+#ifndef OFDM_TX_FAST_BLOCK
+#define OFDM_TX_FAST_BLOCK 512
+#endif
+#ifndef OFDM_RX_FAST_BLOCK
+#define OFDM_RX_FAST_BLOCK 512
+#endif
 
 namespace ofdm {
+
+template <int FB, int LOGN>
+constexpr int tx_block() { return FB > 0 && LOGN <= 10 ? OFDM_TX_FAST_BLOCK : kBlock; }
+template <int FB, int LOGN, int EQ>
+constexpr int rx_block() { return FB > 0 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock; }
+constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 
 // Reference mode: stage OFDM symbol s's tx bits from the packed bytes of the run
 // (symbol s starts at bit s*bps, zeros past the end) as 32-bit words in W
@@ -70,15 +85,24 @@ __device__ __forceinline__ cpx<R> mmse_coef(cpx<R> hc, R h2, R nv) {
 }
 
 // Per-element tx constellation indices of one symbol for this lane, from whichever
-// source the launch uses: the lane's Philox block (philox mode) or the staged words
-// (reference mode).  FB > 0: fixed b = FB, compile-time offsets.
+// source the launch uses: the lane generator's first 128 bits (philox mode) or the
+// staged words (reference mode).  FB > 0: fixed b = FB, compile-time offsets.  In philox
+// mode the generator g continues into the lane's noise (RX).
 template <int FB, int TPS>
 struct TxBits {
     u4 lane;
+    Sfc32 g;
     const uint32_t* W;
     int base_bit;
     bool from_words;
 
+    __device__ __forceinline__ void seed_lane(uint64_t seed, int64_t s, int t) {
+        g.seed(philox_lane(seed, s, (uint32_t)t, kLane));
+        lane.x = g.next();
+        lane.y = g.next();
+        lane.z = g.next();
+        lane.w = g.next();
+    }
     __device__ __forceinline__ void load(const TxRxCommon& a, int64_t s, int t, uint32_t* Wslot, bool active) {
         from_words = FB == 0 && a.bits != nullptr;
         W = Wslot;
@@ -87,18 +111,18 @@ struct TxBits {
         if (from_words) {
             if (active) base_bit = stage_words<TPS>(a, s, Wslot, t);
         } else if (active) {
-            lane = philox_lane(a.seed, s, (uint32_t)t, kLaneBits);
+            seed_lane(a.seed, s, t);
         }
     }
     template <int I>
     __device__ __forceinline__ uint32_t fixed() const {
-        return bits128_c<FB * I, FB>(lane);
+        return lane_bits(lane, I, FB);
     }
-    // lane_off: running offset over this lane's active elements (philox mode);
-    // stream_off: the element's offset inside the symbol's stream (reference mode)
-    __device__ __forceinline__ uint32_t generic(int lane_off, int b, int stream_off) const {
+    // i: the element's index in the lane (philox mode); stream_off: its offset inside the
+    // symbol's bit stream (reference mode)
+    __device__ __forceinline__ uint32_t generic(int i, int b, int stream_off) const {
         if (from_words) return extract_w(W, base_bit + stream_off, b);
-        return bits128(lane, lane_off, b);
+        return lane_bits(lane, i, b);
     }
 };
 
@@ -115,8 +139,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 // stream samples of the previous symbol) is carried in LDS; the first symbol of a chunk
 // regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
 template <typename R, int LOGN, int FB>
-__global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
-    using G = Geo<LOGN>;
+__global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, LOGN>(), OFDM_TX_WAVES))) void k_tx(
+    TxArgs a) {
+    constexpr int BLK = tx_block<FB, LOGN>();
+    using G = Geo<LOGN, BLK>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
     const TxRxCommon& cm = a.c;
@@ -125,17 +151,21 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
     const int slot = a.slot;  // complex elements per symbol row (>= PADN and >= L-1+cp+N)
     const int tls = L > 1 ? L - 1 : 1;
     Carve cv(ofdm_smem);
-    C* tw = cv.take<C>(128);
+    C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
     C* lut = cv.take<C>(cm.lut_len);
     C* h = cv.take<C>(32);
     AxisInfo* axis = cv.take<AxisInfo>(4);
     C* rows = cv.take<C>((size_t)G::SPB * slot);
     C* tails = cv.take<C>((size_t)G::SPB * tls);
-    uint32_t* words = cv.take<uint32_t>((size_t)G::SPB * cm.words_per_sym);
-    double* red = cv.take<double>(kBlock / 64);
+    uint32_t* words = cv.take<uint32_t>(FB ? 0 : (size_t)G::SPB * cm.words_per_sym);  // reference bits
+    double* red = cv.take<double>(BLK / 64);
+    constexpr int TTS = FB ? tt_size(LOGN) : 0;
+    C* tt = cv.take<C>(TTS);  // throughput kernel: inverse per-pass twiddles
 
-    load_twiddles<R>(tw, (const C*)cm.tw);
-    for (int i = threadIdx.x; i < cm.lut_len; i += kBlock) lut[i] = ((const C*)cm.lut)[i];
+    if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
+    for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
+    // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element)
+    for (int i = threadIdx.x; i < cm.lut_len; i += BLK) lut[i] = cscale(((const C*)cm.lut)[i], (R)cm.scale);
     if (threadIdx.x < L) h[threadIdx.x] = ((const C*)a.h)[threadIdx.x];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     __syncthreads();
@@ -146,7 +176,6 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
     C* tl = tails + ls * tls;
     uint32_t* W = words + ls * cm.words_per_sym;
     C* yout = (C*)a.y;
-    const R scale = (R)cm.scale;
     const C h0 = h[0];
     const int64_t ngroups = (cm.n_sym + a.chunk - 1) / a.chunk;
     const int64_t niter = (ngroups + G::SPB - 1) / G::SPB;
@@ -166,11 +195,8 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
             // 1/sqrt(N) of ifft(norm="ortho") folded in
             C x[E];
             if constexpr (FB > 0) {
-                static_for<0, E>([&](auto I) {
-                    x[I] = active ? cscale(lut[tb.template fixed<I>()], scale) : mk<R>(0, 0);
-                });
+                static_for<0, E>([&](auto I) { x[I] = active ? lut[tb.template fixed<I>()] : mk<R>(0, 0); });
             } else {
-                int loff = 0;
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
                     const int k = t + i * TPS;
@@ -178,46 +204,61 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
                     if (active) {
                         if (adaptive) {
                             const ScInfo sc = cm.sc[k];
-                            if (sc.lut >= 0) {
-                                v = lut[axis[sc.lut].lut_off + tb.generic(loff, sc.bits, sc.bitoff)];
-                                loff += sc.bits;
-                            }
+                            if (sc.lut >= 0) v = lut[axis[sc.lut].lut_off + tb.generic(i, sc.bits, sc.bitoff)];
                         } else {
-                            v = lut[tb.generic(loff, cm.b, k * cm.b)];
-                            loff += cm.b;
+                            v = lut[tb.generic(i, cm.b, k * cm.b)];
                         }
                     }
-                    x[i] = cscale(v, scale);
+                    x[i] = v;
                 }
             }
-            if (!(a.flags & 2)) fft_reg<R, LOGN, true>(x, row, tw, tw + 64, t);
+            if (!(a.flags & 2)) fft_reg<R, LOGN, true, (FB > 0)>(x, row, tw, tw + 64, t, tt);
+            // The prefix repeats samples k >= N - cp.  With cp <= TPS only the lane's last
+            // element can be one of them (one loop-invariant compare); otherwise the compares
+            // are made per symbol against an opaque copy of N - cp, so they are not hoisted
+            // as E live 64-bit masks (SGPR spills).
+            int ncp = N - cp;
+            asm volatile("" : "+s"(ncp));
+            auto prefix_sum = [&](auto&& pw) -> R {
+                if (cp <= TPS) return t >= TPS - cp ? pw(E - 1) : (R)0;
+                R acc = 0;
+#pragma unroll
+                for (int i = 0; i < E; ++i)
+                    if (t + i * TPS >= ncp) acc += pw(i);
+                return acc;
+            };
             // PAPR statistics over the modulated symbol incl. its prefix (simulation/models.py:519-522)
+            R pxs = 0;
             if (active && c >= 0) {
-                R pxs = 0, mxs = 0;  // per-symbol partials in the arithmetic precision
+                R mxs = 0;  // per-symbol partials in the arithmetic precision
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
-                    const int k = t + i * TPS;
                     const R p2 = norm2(x[i]);
-                    pxs += k >= N - cp ? 2 * p2 : p2;
+                    pxs += p2;
                     mxs = fmax(mxs, p2);
                 }
+                pxs += prefix_sum([&](int i) { return norm2(x[i]); });
                 px += pxs;
                 mx = fmax(mx, (double)mxs);
             }
             if (L == 1) {
                 // flat channel: y = h0 x, no inter-symbol memory
                 if (active && c >= 0) {
-                    R pys = 0;
                     C* yo = yout + sl * N;
 #pragma unroll
                     for (int i = 0; i < E; ++i) {
-                        const int k = t + i * TPS;
                         const C yv = cmul(h0, x[i]);
-                        const R p2 = norm2(yv);
-                        pys += k >= N - cp ? 2 * p2 : p2;
-                        if (yout && !(a.flags & 4)) yo[k] = yv;
+                        if (yout && !(a.flags & 4)) yo[t + i * TPS] = yv;
                     }
-                    py += pys;
+                    if constexpr (FB > 0) {
+                        py += (double)(norm2(h0) * pxs);  // |y|^2 = |h0|^2 |x|^2 (complex64 mode)
+                    } else {
+                        R pys = 0;
+#pragma unroll
+                        for (int i = 0; i < E; ++i) pys += norm2(cmul(h0, x[i]));
+                        pys += prefix_sum([&](int i) { return norm2(cmul(h0, x[i])); });
+                        py += pys;
+                    }
                 }
                 sym_sync<TPS>();  // W / row reuse by the next symbol
             } else {
@@ -225,10 +266,15 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
                 sym_sync<TPS>();  // the last FFT pass has read the row
                 const int o = L - 1 + cp;
 #pragma unroll
-                for (int i = 0; i < E; ++i) {
-                    const int k = t + i * TPS;
-                    row[o + k] = x[i];
-                    if (k >= N - cp) row[L - 1 + k - (N - cp)] = x[i];
+                for (int i = 0; i < E; ++i) row[o + t + i * TPS] = x[i];
+                if (cp <= TPS) {
+                    if (t >= TPS - cp) row[L - 1 + t - (TPS - cp)] = x[E - 1];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < E; ++i) {
+                        const int k = t + i * TPS;
+                        if (k >= ncp) row[L - 1 + k - ncp] = x[i];
+                    }
                 }
                 for (int j = t; j < L - 1; j += TPS) row[j] = tl[j];
                 sym_sync<TPS>();
@@ -251,9 +297,9 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
             }
         }
     }
-    py = block_sum<double>(py, red);
-    px = block_sum<double>(px, red);
-    mx = block_max<double>(mx, red);
+    py = block_sum<double, BLK>(py, red);
+    px = block_sum<double, BLK>(px, red);
+    mx = block_max<double, BLK>(mx, red);
     if (threadIdx.x == 0) {
         a.partials[blockIdx.x * 3 + 0] = py;
         a.partials[blockIdx.x * 3 + 1] = px;
@@ -264,22 +310,27 @@ __global__ __launch_bounds__(kBlock, OFDM_TX_WAVES) void k_tx(TxArgs a) {
 // ============================================================ fused RX
 // EQ: OFDM_EQ_* fixed at compile time (throughput kernel) or -1 = from the plan.
 template <typename R, int LOGN, int EQ, int FB>
-__global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
-    using G = Geo<LOGN>;
+__global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<FB, LOGN, EQ>(), OFDM_RX_WAVES))) void k_rx(
+    RxArgs a) {
+    constexpr int BLK = rx_block<FB, LOGN, EQ>();
+    using G = Geo<LOGN, BLK>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
     const TxRxCommon& cm = a.c;
     const int eq = EQ >= 0 ? EQ : cm.eq;
     const bool adaptive = FB ? false : (bool)cm.adaptive;
     Carve cv(ofdm_smem);
-    C* tw = cv.take<C>(128);
+    C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
     AxisInfo* axis = cv.take<AxisInfo>(4);
     C* rows = cv.take<C>((size_t)G::SPB * G::PADN);
-    uint32_t* words = cv.take<uint32_t>((size_t)G::SPB * cm.words_per_sym);
-    R* red = cv.take<R>(kBlock);
-    unsigned long long* redc = cv.take<unsigned long long>(kBlock / 64);
+    uint32_t* words = cv.take<uint32_t>(FB ? 0 : (size_t)G::SPB * cm.words_per_sym);  // reference bits
+    R* red = cv.take<R>(BLK / 64);
+    unsigned long long* redc = cv.take<unsigned long long>(BLK / 64);
+    constexpr int TTS = FB ? tt_size(LOGN) : 0;
+    C* tt = cv.take<C>(TTS);  // throughput kernel: forward per-pass twiddles
 
-    load_twiddles<R>(tw, (const C*)cm.tw);
+    if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
+    for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     __syncthreads();
 
@@ -293,7 +344,11 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
     const int cp = cm.cp;
     const R scale = (R)cm.scale;
     Slicer<R> slicer;
-    if (!adaptive) slicer.load(axis[0]);
+    PermSlicer<FB ? FB : 2> pslicer;
+    if constexpr (FB > 0)
+        pslicer.load(axis[0], (float)cm.scale);  // the FFT output stays unscaled
+    else if (!adaptive)
+        slicer.load(axis[0]);
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     R sigma = 0;
@@ -311,13 +366,17 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
         const int64_t sg = cm.sym0 + sl;
         const bool active = sl < cm.n_sym;
         TxBits<FB, TPS> tb;
-        tb.load(cm, sg, t, W, active && !(a.flags & 4));
+        tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
         // kept channel samples + AWGN; the 1/sqrt(N) of fft(norm="ortho") folded in
         const C* ys = (const C*)a.y + sl * N;
         C x[E];
+        if (active && !(a.flags & 16)) {
 #pragma unroll
-        for (int i = 0; i < E; ++i)
-            x[i] = (active && !(a.flags & 16)) ? ys[t + i * TPS] : mk<R>(0, 0);
+            for (int i = 0; i < E; ++i) x[i] = ys[t + i * TPS];
+        } else {
+#pragma unroll
+            for (int i = 0; i < E; ++i) x[i] = mk<R>(0, 0);
+        }
         if (active && array_noise) {
             const double* nr = a.nr + sg * (N + cp) + cp;
             const double* ni = a.ni + sg * (N + cp) + cp;
@@ -327,19 +386,30 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
                 x[i].im += sigma * (R)ni[t + i * TPS];
             }
         } else if (active && noise) {
-            Xoshiro128ss g;
-            g.seed(philox_lane(cm.seed, sg, (uint32_t)t, kLaneNoise));
+            const float m2s2ln2 = -1.3862943611198906f * (float)sigma * (float)sigma;
+            static_assert(E % 2 == 0 || E == 1, "noise pairs");
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                float nre, nim;
-                g.normal2(nre, nim);
-                x[i].re += sigma * (R)nre;
-                x[i].im += sigma * (R)nim;
+            for (int i = 0; i + 1 < E; i += 2) {
+                if constexpr (sizeof(R) == 4) {
+                    tb.g.add_noise2(x[i].v, x[i + 1].v, m2s2ln2);
+                } else {
+                    f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
+                    tb.g.add_noise2(n0, n1, m2s2ln2);
+                    x[i] = x[i] + mk<R>((R)n0.x, (R)n0.y);
+                    x[i + 1] = x[i + 1] + mk<R>((R)n1.x, (R)n1.y);
+                }
+            }
+            if constexpr (E == 1) {
+                f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
+                tb.g.add_noise2(n0, n1, m2s2ln2);
+                x[0] = x[0] + mk<R>((R)n0.x, (R)n0.y);
             }
         }
+        if constexpr (FB == 0) {
 #pragma unroll
-        for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
-        if (!(a.flags & 2)) fft_reg<R, LOGN, false>(x, row, tw, tw + 64, t);
+            for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
+        }
+        if (!(a.flags & 2)) fft_reg<R, LOGN, false, (FB > 0)>(x, row, tw, tw + 64, t, tt);
         if (FB == 0) sym_sync<TPS>();  // staged words visible to the whole group
         // MMSE noise variance per OFDM symbol (equalization/models.py:39-49)
         R nv = 0;
@@ -348,14 +418,14 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
 #pragma unroll
             for (int i = 0; i < E; ++i) p += norm2(x[i]);
             p = group_sum<R, TPS>(p, red);
+            if constexpr (FB > 0) p *= scale * scale;  // power of the ortho-scaled spectrum
             nv = cm.gain_mean == 0.0 ? (R)INFINITY : ((p / (R)N) / (R)a.snr_lin) / (R)cm.gain_mean;
         }
         if (active && !(a.flags & 8)) {
             const int64_t sbit = sg * cm.bps;
             const bool all_valid = FB > 0 || sbit + cm.bps <= a.n_valid_bits;
             uint32_t bes = 0, ses = 0;
-            int loff = 0;
-            auto element = [&](int i, uint32_t tidx_fixed) {
+            auto equalized = [&](int i) {
                 const int k = t + i * TPS;
                 C v = x[i];
                 if (eq == OFDM_EQ_ZF) {
@@ -363,51 +433,55 @@ __global__ __launch_bounds__(kBlock, OFDM_RX_WAVES) void k_rx(RxArgs a) {
                 } else if (eq == OFDM_EQ_MMSE) {
                     v = cmul(v, mmse_coef<R>(eqa[k], eqb[k], nv));
                 }
-                if (FB == 0 && sl < a.z_keep) ((C*)a.z_out)[sl * N + k] = v;
-                uint32_t ridx, tidx;
-                int b, off;
-                if (FB > 0) {
-                    b = FB;
-                    off = k * FB;
-                    ridx = slicer(v);
-                    tidx = tidx_fixed;
-                } else if (adaptive) {
-                    const ScInfo sc = cm.sc[k];
-                    if (sc.lut < 0) return;
-                    b = sc.bits;
-                    off = sc.bitoff;
-                    ridx = slice<R>(v, axis[sc.lut]);
-                    tidx = tb.generic(loff, b, off);
-                    loff += b;
-                } else {
-                    b = cm.b;
-                    off = k * b;
-                    ridx = slicer(v);
-                    tidx = tb.generic(loff, b, off);
-                    loff += b;
-                }
-                uint32_t d = ridx ^ tidx;
-                ses += d != 0u;
-                if (!all_valid) {
-                    const int64_t nvb = a.n_valid_bits - (sbit + off);
-                    const int keep = nvb <= 0 ? 0 : (nvb >= b ? b : (int)nvb);
-                    d &= ((1u << keep) - 1u) << (b - keep);
-                }
-                bes += __popc(d);
+                return v;
             };
             if constexpr (FB > 0) {
-                static_for<0, E>([&](auto I) { element(I, tb.template fixed<I>()); });
+                // four elements per lane word: slice, look up, compare, count
+                static_for<0, E / 4>([&](auto Q) {
+                    constexpr int q = Q;
+                    C z[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
+                    const uint32_t d = pslicer.diff(z, lane_word(tb.lane, q));
+                    bes += __popc(d);
+                    ses += PermSlicer<FB ? FB : 2>::nonzero_bytes(d);
+                });
             } else {
 #pragma unroll
-                for (int i = 0; i < E; ++i) element(i, 0u);
+                for (int i = 0; i < E; ++i) {
+                    const int k = t + i * TPS;
+                    const C v = equalized(i);
+                    if (sl < a.z_keep) ((C*)a.z_out)[sl * N + k] = v;
+                    uint32_t ridx;
+                    int b, off;
+                    if (adaptive) {
+                        const ScInfo sc = cm.sc[k];
+                        if (sc.lut < 0) continue;
+                        b = sc.bits;
+                        off = sc.bitoff;
+                        ridx = slice<R>(v, axis[sc.lut]);
+                    } else {
+                        b = cm.b;
+                        off = k * b;
+                        ridx = slicer(v);
+                    }
+                    uint32_t d = ridx ^ tb.generic(i, b, off);
+                    ses += d != 0u;
+                    if (!all_valid) {
+                        const int64_t nvb = a.n_valid_bits - (sbit + off);
+                        const int keep = nvb <= 0 ? 0 : (nvb >= b ? b : (int)nvb);
+                        d &= ((1u << keep) - 1u) << (b - keep);
+                    }
+                    bes += __popc(d);
+                }
             }
             be += bes;
             se += ses;
         }
         sym_sync<TPS>();  // W and the FFT row are rewritten by the next symbol
     }
-    be = block_sum<unsigned long long>(be, redc);
-    se = block_sum<unsigned long long>(se, redc);
+    be = block_sum<unsigned long long, BLK>(be, redc);
+    se = block_sum<unsigned long long, BLK>(se, redc);
     if (threadIdx.x == 0) {
         if (be) atomicAdd((unsigned long long*)&a.counters[0], be);
         if (se) atomicAdd((unsigned long long*)&a.counters[1], se);

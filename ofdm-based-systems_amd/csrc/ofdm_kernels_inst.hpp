@@ -102,19 +102,22 @@ hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
 }
 
 template <typename R, int LOGN, int FB>
-static hipError_t tx_launch(const TxArgs& a, int grid, hipStream_t s) {
-    const size_t sm = smem_tx<R>(LOGN, a.c.lut_len, a.c.words_per_sym, a.L, a.c.cp);
+static hipError_t tx_launch(const TxArgs& a, int* grid, hipStream_t s) {
+    constexpr int BLK = tx_block<FB, LOGN>();
+    const size_t sm = smem_tx<R>(LOGN, BLK, a.c.lut_len, a.c.words_per_sym, a.L, a.c.cp, FB ? tt_size(LOGN) : 0);
     auto fn = k_tx<R, LOGN, FB>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), sm, s, a);
+    const int64_t groups = (a.c.n_sym + a.chunk - 1) / a.chunk;
+    *grid = clamp_grid((groups + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
+    hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
 
 // Throughput configuration (complex64, fixed square QAM, Philox bits; N >= 64) -> the
 // kernel specialised on the bits per subcarrier; anything else -> the generic kernel.
 template <typename R, int LOGN>
-static hipError_t tx_one(const TxArgs& a, int grid, hipStream_t s) {
+static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (!a.c.adaptive && a.c.bits == nullptr) {
             switch (a.c.b) {
@@ -130,7 +133,7 @@ static hipError_t tx_one(const TxArgs& a, int grid, hipStream_t s) {
 }
 
 template <typename R>
-hipError_t launch_tx(int logn, const TxArgs& a, int grid, hipStream_t s) {
+hipError_t launch_tx(int logn, const TxArgs& a, int* grid, hipStream_t s) {
 #define OFDM_TX_CASE(L) \
     case L:             \
         return tx_one<R, L>(a, grid, s);
@@ -143,17 +146,19 @@ hipError_t launch_tx(int logn, const TxArgs& a, int grid, hipStream_t s) {
 }
 
 template <typename R, int LOGN, int EQ, int FB>
-static hipError_t rx_launch(const RxArgs& a, int grid, hipStream_t s) {
-    const size_t sm = smem_rx<R>(LOGN, a.c.words_per_sym);
+static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
+    constexpr int BLK = rx_block<FB, LOGN, EQ>();
+    const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym, FB ? tt_size(LOGN) : 0);
     auto fn = k_rx<R, LOGN, EQ, FB>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), sm, s, a);
+    *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
+    hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
 
 template <typename R, int LOGN, int FB>
-static hipError_t rx_eq(const RxArgs& a, int grid, hipStream_t s) {
+static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
     if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, FB>(a, grid, s);
     if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, FB>(a, grid, s);
     return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB>(a, grid, s);
@@ -163,7 +168,7 @@ static hipError_t rx_eq(const RxArgs& a, int grid, hipStream_t s) {
 // received-symbol tap; N >= 64) -> kernel specialised on bits and equaliser; anything
 // else -> the generic kernel.
 template <typename R, int LOGN>
-static hipError_t rx_one(const RxArgs& a, int grid, hipStream_t s) {
+static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr) {
             switch (a.c.b) {
@@ -179,7 +184,7 @@ static hipError_t rx_one(const RxArgs& a, int grid, hipStream_t s) {
 }
 
 template <typename R>
-hipError_t launch_rx(int logn, const RxArgs& a, int grid, hipStream_t s) {
+hipError_t launch_rx(int logn, const RxArgs& a, int* grid, hipStream_t s) {
 #define OFDM_RX_CASE(L) \
     case L:             \
         return rx_one<R, L>(a, grid, s);
@@ -199,7 +204,7 @@ hipError_t launch_rx(int logn, const RxArgs& a, int grid, hipStream_t s) {
     template hipError_t launch_conv<R>(const ConvArgs&, int, hipStream_t);          \
     template hipError_t launch_power<R>(const PowerArgs&, int, hipStream_t);        \
     template hipError_t launch_awgn<R>(const AwgnArgs&, hipStream_t);               \
-    template hipError_t launch_tx<R>(int, const TxArgs&, int, hipStream_t);         \
-    template hipError_t launch_rx<R>(int, const RxArgs&, int, hipStream_t);
+    template hipError_t launch_tx<R>(int, const TxArgs&, int*, hipStream_t);         \
+    template hipError_t launch_rx<R>(int, const RxArgs&, int*, hipStream_t);
 
 }  // namespace ofdm

@@ -87,6 +87,7 @@ struct TxRxCommon {
     uint64_t seed;
     int64_t sym0, n_sym;
     const void* tw;
+    const void* ptw;  // per-pass twiddle tables [forward | inverse], tt_size(logn) each
     const void* lut;
     int lut_len;
     const AxisInfo* axis;
@@ -129,11 +130,11 @@ struct RxArgs {
 
 // ---- LDS footprints (must mirror the Carve sequences in ofdm_kernels.hpp)
 inline size_t rnd16(size_t n) { return (n + 15) & ~size_t(15); }
-inline int geo_spb(int logn) {
+inline int geo_spb(int logn, int blk = 256) {
     const int loge = logn < 4 ? logn : 4;
-    return 256 / ((1 << logn) >> loge);
+    return blk / ((1 << logn) >> loge);
 }
-inline int geo_padn(int logn) { return (1 << logn) + ((1 << logn) >> 4) + 1; }
+inline int geo_padn(int logn) { return (1 << logn) + ((1 << logn) >> 4); }
 
 template <typename R>
 inline size_t smem_rows(int logn) {
@@ -146,21 +147,26 @@ inline int tx_slot(int logn, int cp, int L) {
     const int ext = (1 << logn) + cp + (L > 1 ? L - 1 : 0);
     return geo_padn(logn) > ext ? geo_padn(logn) : ext;
 }
+// fused kernels, blk threads; tts = per-pass twiddle entries (throughput kernels) or 0
+// (the throughput kernels, tts > 0, carve no two-level twiddles and no staged bit words)
 template <typename R>
-inline size_t smem_tx(int logn, int lut_len, int wps, int L, int cp) {
+inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int cp, int tts) {
     const size_t c = 2 * sizeof(R);
-    const int spb = geo_spb(logn);
+    const int spb = geo_spb(logn, blk);
     const int tls = L > 1 ? L - 1 : 1;
-    return rnd16(128 * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(4 * sizeof(AxisInfo)) +
+    if (tts > 0) wps = 0;
+    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(4 * sizeof(AxisInfo)) +
            rnd16((size_t)spb * tx_slot(logn, cp, L) * c) + rnd16((size_t)spb * tls * c) +
-           rnd16((size_t)spb * wps * 4) + rnd16(4 * sizeof(double));
+           rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(double)) + rnd16((size_t)tts * c);
 }
 template <typename R>
-inline size_t smem_rx(int logn, int wps) {
+inline size_t smem_rx(int logn, int blk, int wps, int tts) {
     const size_t c = 2 * sizeof(R);
-    const int spb = geo_spb(logn);
-    return rnd16(128 * c) + rnd16(4 * sizeof(AxisInfo)) + rnd16((size_t)spb * geo_padn(logn) * c) +
-           rnd16((size_t)spb * wps * 4) + rnd16(256 * sizeof(R)) + rnd16(4 * sizeof(unsigned long long));
+    const int spb = geo_spb(logn, blk);
+    if (tts > 0) wps = 0;
+    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16(4 * sizeof(AxisInfo)) + rnd16((size_t)spb * geo_padn(logn) * c) +
+           rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(R)) +
+           rnd16((size_t)(blk / 64) * sizeof(unsigned long long)) + rnd16((size_t)tts * c);
 }
 
 // ---- launchers (instantiated for float and double in ofdm_kernels_f{32,64}.hip)
@@ -178,10 +184,11 @@ template <typename R>
 hipError_t launch_power(const PowerArgs& a, int grid, hipStream_t s);
 template <typename R>
 hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s);
+// the fused launchers pick the kernel (and its workgroup size) and return the grid used
 template <typename R>
-hipError_t launch_tx(int logn, const TxArgs& a, int grid, hipStream_t s);
+hipError_t launch_tx(int logn, const TxArgs& a, int* grid, hipStream_t s);
 template <typename R>
-hipError_t launch_rx(int logn, const RxArgs& a, int grid, hipStream_t s);
+hipError_t launch_rx(int logn, const RxArgs& a, int* grid, hipStream_t s);
 
 hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int max_mask,
                            double* stats, hipStream_t s);

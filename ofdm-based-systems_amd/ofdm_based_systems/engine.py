@@ -109,11 +109,18 @@ class LinkEngine:
                                   int(z_keep)))
 
     # ------------------------------------------------------------------ run
-    def run(self, n_sym: int, snr_db: float, *, bits: Optional[np.ndarray] = None,
-            normals: Optional[tuple] = None, seed: int = 0, noise_on: bool = True, keep_symbols: int = 0,
-            group=None, y_budget: int = DEFAULT_Y_BUDGET, batch: Optional[int] = None,
-            n_valid_bits: Optional[int] = None, events: Optional[list] = None) -> LinkStats:
-        """Simulate global OFDM symbols [0, n_sym) (this rank's shard when ``group`` is set).
+    def run(self, n_sym: int, snr_db: float, **kw) -> LinkStats:
+        """Simulate global OFDM symbols [0, n_sym) and return the counts (see :meth:`run_async`)."""
+        return self.run_async(n_sym, snr_db, **kw).result()
+
+    def run_async(self, n_sym: int, snr_db: float, *, bits: Optional[np.ndarray] = None,
+                  normals: Optional[tuple] = None, seed: int = 0, noise_on: bool = True, keep_symbols: int = 0,
+                  group=None, y_budget: int = DEFAULT_Y_BUDGET, batch: Optional[int] = None,
+                  n_valid_bits: Optional[int] = None, events: Optional[list] = None) -> "PendingLink":
+        """Enqueue global OFDM symbols [0, n_sym) (this rank's shard when ``group`` is set) on
+        the current stream without waiting for them; :meth:`PendingLink.result` reads the
+        counts back.  Back-to-back calls therefore keep the GPU busy while the host prepares
+        the next batch.
 
         bits    : packed tx bytes of the whole run (reference mode) or None (Philox)
         normals : (nr, ni) float64 arrays of length n_sym*(N+cp) (reference mode), or None
@@ -187,12 +194,25 @@ class LinkEngine:
             import torch.distributed as dist
 
             dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
-        st = stats.cpu().numpy()
-        cnt = counters.cpu().numpy()
+        return PendingLink(n_sym, samples, stats, counters, z_out)
+
+
+class PendingLink:
+    """Device-side results of one :meth:`LinkEngine.run_async` call."""
+
+    def __init__(self, n_sym, samples, stats, counters, z_out):
+        self.n_sym, self.samples = n_sym, samples
+        self.stats, self.counters, self.z_out = stats, counters, z_out
+
+    def result(self) -> LinkStats:
+        st = self.stats.cpu().numpy()
+        cnt = self.counters.cpu().numpy()
+        samples = self.samples
         avg = st[1] / samples if samples else 0.0
         papr = float(10 * np.log10(st[2] / avg)) if avg > 0 else float("inf")
+        z = self.z_out
         return LinkStats(
-            bit_errors=int(cnt[0]), symbol_errors=int(cnt[1]), num_ofdm_symbols=n_sym,
+            bit_errors=int(cnt[0]), symbol_errors=int(cnt[1]), num_ofdm_symbols=self.n_sym,
             power_sum=float(st[0]), x_power_sum=float(st[1]), x_peak=float(st[2]), samples=samples,
-            papr_db=papr, received=None if z_out is None else z_out.cpu().numpy().reshape(-1),
+            papr_db=papr, received=None if z is None else z.cpu().numpy().reshape(-1),
         )
