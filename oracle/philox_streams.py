@@ -1,0 +1,164 @@
+"""Throughput-mode ("philox") streams and link restated on the CPU -- TEST INFRASTRUCTURE ONLY.
+
+The reference draws its payload bits from PCG64 and its noise from NumPy's legacy normal
+generator; ``ofdm_oracle.reference_streams`` reproduces those exactly.  The build's
+throughput mode instead generates bits and noise inside the fused kernels from a
+counter-based definition (``ofdm-based-systems_amd/csrc/ofdm_device.hpp``, section
+"throughput-mode streams"), so that a run needs no host data and does not depend on how
+symbols are batched or sharded.  This module restates that definition in NumPy and runs
+the link through the oracle's arithmetic (``ofdm_oracle``: modulate, channel, equalise,
+nearest-point decision -- the functions pinned to the reference's golden vectors), so the
+fused throughput kernels are checked against the oracle on identical bits and noise.
+
+Like ``ofdm_oracle`` it is the CHECKER: only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it.
+
+Definition (one OFDM symbol s of N subcarriers, E = min(16, N) elements per lane,
+TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS for i < E):
+
+* lane generator: SFC32 (a, b, c, counter starting at 1) seeded with words 0..2 of one
+  Philox4x32-10 block, key = (seed mod 2^32, seed >> 32), counter = (t, s mod 2^32,
+  s >> 32, 0x1A7E5EED);
+* payload: outputs 0..3 are 128 bits; element i takes the low b bits of byte i (byte i =
+  bits 8*(i & 3).. of output i >> 2);
+* noise: outputs 4+3j, 5+3j, 6+3j give elements 2j, 2j+1: radius words u0, u1, angle word
+  a; element 2j+q gets sigma*sqrt(-2 ln((u_q + 0.5) 2^-32)) * exp(2 pi i v_q) with
+  v_0 = (a >> 16) 2^-16, v_1 = (a & 0xffff) 2^-16, added to the kept time sample k.
+  (float32 arithmetic on the GPU; here the radius argument follows the same float32
+  rounding and the rest is evaluated in float64.)
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+import ofdm_oracle as O  # oracle/ is on the path of its callers (tests, smoke, bench)
+
+PHILOX_M0 = np.uint64(0xD2511F53)
+PHILOX_M1 = np.uint64(0xCD9E8D57)
+PHILOX_W0 = 0x9E3779B9
+PHILOX_W1 = 0xBB67AE85
+K_LANE = 0x1A7E5EED
+MASK32 = np.uint64(0xFFFFFFFF)
+
+
+def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
+    """Philox4x32-10 (Salmon et al., SC'11; Random123 reference): 10 rounds of
+    (hi(M0 c0) ^ c3 ^ k1 ... ) bijections keyed by the Weyl sequence k += W."""
+    c = [np.asarray(v, dtype=np.uint64) & MASK32 for v in (c0, c1, c2, c3)]
+    k0, k1 = int(k0) & 0xFFFFFFFF, int(k1) & 0xFFFFFFFF
+    for _ in range(10):
+        p0 = PHILOX_M0 * c[0]
+        p1 = PHILOX_M1 * c[2]
+        c = [((p1 >> np.uint64(32)) ^ c[1] ^ np.uint64(k0)) & MASK32, p1 & MASK32,
+             ((p0 >> np.uint64(32)) ^ c[3] ^ np.uint64(k1)) & MASK32, p0 & MASK32]
+        k0 = (k0 + PHILOX_W0) & 0xFFFFFFFF
+        k1 = (k1 + PHILOX_W1) & 0xFFFFFFFF
+    return [v.astype(np.uint32) for v in c]
+
+
+class Sfc32:
+    """SFC32 (Doty-Humphrey, PractRand): tmp = a + b + counter; a = b ^ (b >> 9);
+    b = c + (c << 3); c = rotl(c, 21) + tmp.  Vectorised over lanes; counter from 1."""
+
+    def __init__(self, a, b, c):
+        self.a, self.b, self.c = (np.asarray(v, np.uint32).copy() for v in (a, b, c))
+        self.n = np.uint32(0)
+
+    def next(self) -> np.ndarray:
+        with np.errstate(over="ignore"):
+            self.n = np.uint32(self.n + np.uint32(1))
+            r = self.a + self.b + self.n
+            self.a = self.b ^ (self.b >> np.uint32(9))
+            self.b = self.c + (self.c << np.uint32(3))
+            self.c = ((self.c << np.uint32(21)) | (self.c >> np.uint32(11))) + r
+        return r
+
+
+def geometry(N: int):
+    E = min(16, N)
+    return E, N // E
+
+
+def lane_generators(seed: int, s: np.ndarray, N: int) -> Sfc32:
+    """One SFC32 per (symbol, lane), lanes in row-major (s, t) order."""
+    E, tps = geometry(N)
+    s = np.asarray(s, dtype=np.int64)
+    ss = np.repeat(s, tps).astype(np.uint64)
+    t = np.tile(np.arange(tps, dtype=np.uint64), len(s))
+    x, y, z, _ = philox4x32_10(t, ss & MASK32, ss >> np.uint64(32), np.full_like(t, K_LANE),
+                               seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return Sfc32(x, y, z)
+
+
+def _lane_to_row(v: np.ndarray, S: int, N: int) -> np.ndarray:
+    """(S*TPS, E) lane-major values -> (S, N) in subcarrier / time-sample order."""
+    E, tps = geometry(N)
+    return v.reshape(S, tps, E).transpose(0, 2, 1).reshape(S, N)
+
+
+def tx_indices(gen: Sfc32, S: int, N: int, b: int) -> np.ndarray:
+    """Constellation indices (S, N) from outputs 0..3 of every lane generator."""
+    E, _ = geometry(N)
+    words = np.stack([gen.next() for _ in range(4)], axis=1)  # (lanes, 4)
+    i = np.arange(E)
+    idx = (words[:, i >> 2] >> (8 * (i & 3)).astype(np.uint32)) & np.uint32((1 << b) - 1)
+    return _lane_to_row(idx.astype(np.int64), S, N)
+
+
+def lane_noise(gen: Sfc32, S: int, N: int, sigma: float) -> np.ndarray:
+    """Complex noise (S, N) at the kept time samples, from outputs 4.. of every lane."""
+    E, _ = geometry(N)
+    sig = np.float32(sigma)
+    m2s2ln2 = np.float32(-1.3862943611198906) * sig * sig  # -2 ln2 sigma^2 in float32
+    cols = []
+    for _ in range((E + 1) // 2):
+        u = [gen.next(), gen.next()]
+        a = gen.next()
+        v = [(a >> np.uint32(16)).astype(np.float64) * 2.0 ** -16, (a & np.uint32(0xFFFF)).astype(np.float64) * 2.0 ** -16]
+        for q in range(2):
+            uf = (u[q].astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -32)
+            r = np.sqrt(np.float64(m2s2ln2) * np.log2(uf.astype(np.float64)))
+            cols.append(r * np.exp(2j * np.pi * v[q]))
+    n = np.stack(cols[:E], axis=1)
+    return _lane_to_row(n, S, N)
+
+
+@dataclass
+class PhiloxLink:
+    bit_errors: int
+    symbol_errors: int
+    power_sum: float
+    x_power_sum: float
+    x_peak: float
+    idx: np.ndarray        # (S, N) tx constellation indices
+    y: np.ndarray          # (S, N) kept channel samples (before noise)
+
+
+def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq: str, snr_db: float,
+               noise_on: bool = True) -> PhiloxLink:
+    """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic."""
+    b = int(np.log2(M))
+    lut = O.qam_lut(M)
+    gen = lane_generators(seed, np.arange(S), N)
+    idx = tx_indices(gen, S, N, b)
+    x = O.modulate(lut[idx], cp)                       # (S, N+cp) incl. prefix
+    px = float(np.sum(np.abs(x) ** 2))
+    mx = float(np.max(np.abs(x) ** 2))
+    y = O.channel_conv(x.ravel(), np.asarray(h_raw, np.complex128))
+    py = float(np.sum(np.abs(y) ** 2))
+    yk = y.reshape(S, N + cp)[:, cp:]
+    rxs = yk.copy()
+    if noise_on:
+        p = py / (S * (N + cp))
+        sigma = np.sqrt((p / 10 ** (snr_db / 10)) / 2.0)
+        rxs = rxs + lane_noise(gen, S, N, sigma)
+    H = np.fft.fft(np.asarray(h_raw, np.complex128), N)
+    Z = O.equalize(np.fft.fft(rxs, axis=1, norm="ortho"), H, eq, snr_db)
+    ridx = O.nn_demap(Z.ravel(), lut).reshape(S, N)
+    diff = (ridx ^ idx).astype(np.uint64)
+    be = int(sum(int(np.count_nonzero((diff >> np.uint64(j)) & np.uint64(1))) for j in range(b)))
+    se = int(np.count_nonzero(ridx != idx))
+    return PhiloxLink(be, se, py, px, mx, idx, yk)

@@ -1,0 +1,99 @@
+"""Throughput mode against the oracle on identical inputs.
+
+The fused kernels generate their bits and noise from the throughput-mode stream
+definition; oracle/philox_streams.py restates that definition and runs the link through
+the oracle's (reference-pinned) arithmetic.  Checked here, per configuration:
+
+* TX: the kept channel samples y of the complex64 kernel vs the oracle's modulate +
+  channel on the same bits (relative 1e-4 of the rms sample: float32 IFFT/FIR rounding),
+  and the power / PAPR statistics (relative 1e-5);
+* RX: bit and symbol error counts vs the oracle's on the same bits and noise.  The GPU
+  computes in float32 with the hardware transcendentals, the oracle in float64, so a
+  decision can differ only for received points within ~1e-6 of a boundary: the counts
+  must agree to 3 + 0.1 %.
+
+Sizes cover both workgroup shapes of the throughput kernels (512 threads at N <= 1024
+without equaliser, 256 otherwise), the multipath FIR, all three equalisers, QPSK to
+256-QAM, and the generic kernel in throughput mode (N < 64 and complex128).
+"""
+
+import numpy as np
+import pytest
+import torch
+from conftest import channel
+
+import philox_streams as P
+import ofdm_oracle as O
+from ofdm_based_systems import _backend as B
+from ofdm_based_systems.engine import LinkEngine
+
+pytestmark = pytest.mark.gpu
+
+EQ = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}
+
+# N, M, channel, equaliser, OFDM symbols, SNR dB (BER ~1e-3 .. 1e-2), precision
+CASES = [
+    (1024, 64, "flat_fading", "NONE", 512, 20.0, B.OFDM_F32),
+    (1024, 64, "severe_multipath", "MMSE", 512, 24.0, B.OFDM_F32),
+    (256, 16, "Lin-Phoong_P1", "ZF", 1024, 22.0, B.OFDM_F32),
+    (64, 4, "rayleigh_fading", "ZF", 4096, 14.0, B.OFDM_F32),
+    (4096, 256, "Lin-Phoong_P1", "MMSE", 96, 31.0, B.OFDM_F32),
+    (2048, 16, "flat_fading", "NONE", 256, 14.0, B.OFDM_F32),
+    (32, 16, "flat_fading", "NONE", 8192, 14.0, B.OFDM_F32),
+    (1024, 64, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F64),
+]
+IDS = [f"N{c[0]}-M{c[1]}-{c[2]}-{c[3]}-{'f32' if c[6] == B.OFDM_F32 else 'f64'}" for c in CASES]
+
+
+def setup(N, M, ch, eq, prec):
+    h = channel(ch)
+    cp = len(h) - 1
+    return LinkEngine(N, cp, h, EQ[eq], [O.qam_lut(M)], None, prec), h, cp
+
+
+@pytest.mark.parametrize("N,M,ch,eq,S,snr,prec", CASES, ids=IDS)
+def test_tx_samples_match_oracle(gpu, N, M, ch, eq, S, snr, prec):
+    eng, h, cp = setup(N, M, ch, eq, prec)
+    seed = 1234
+    y = torch.empty((S, N), dtype=eng.cdtype, device="cuda")
+    stats = torch.zeros(3, dtype=torch.float64, device="cuda")
+    eng.tx(eng.stream(), None, seed, 0, S, y, stats)
+    torch.cuda.synchronize()
+    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, noise_on=False)
+    got = y.cpu().numpy()
+    rms = np.sqrt(np.mean(np.abs(ref.y) ** 2))
+    tol = 1e-4 if prec == B.OFDM_F32 else 1e-12
+    assert np.max(np.abs(got - ref.y)) <= tol * rms
+    st = stats.cpu().numpy()
+    rt = 1e-5 if prec == B.OFDM_F32 else 1e-12
+    assert st[0] == pytest.approx(ref.power_sum, rel=rt)
+    assert st[1] == pytest.approx(ref.x_power_sum, rel=rt)
+    assert st[2] == pytest.approx(ref.x_peak, rel=rt)
+
+
+@pytest.mark.parametrize("N,M,ch,eq,S,snr,prec", CASES, ids=IDS)
+def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec):
+    eng, h, cp = setup(N, M, ch, eq, prec)
+    seed = 77
+    res = eng.run(S, snr, seed=seed)
+    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr)
+    assert ref.bit_errors > 100, "SNR too high for a meaningful count"
+    for got, want in ((res.bit_errors, ref.bit_errors), (res.symbol_errors, ref.symbol_errors)):
+        assert abs(got - want) <= 3 + 1e-3 * want, (got, want)
+    assert res.power_sum == pytest.approx(ref.power_sum, rel=1e-5)
+
+
+def test_sharded_halves_add_up_to_the_whole(gpu):
+    """Symbols [0, S) in two launches at different offsets = one launch (stream is per symbol)."""
+    eng, h, cp = setup(1024, 64, "severe_multipath", "MMSE", B.OFDM_F32)
+    S = 600
+    whole = eng.run(S, 24.0, seed=9)
+    y = torch.empty((S, 1024), dtype=eng.cdtype, device="cuda")
+    st = torch.zeros(3, dtype=torch.float64, device="cuda")
+    eng.tx(eng.stream(), None, 9, 0, 250, y[:250], st)
+    eng.tx(eng.stream(), None, 9, 250, S - 250, y[250:], st)
+    y2 = torch.empty_like(y)
+    eng.tx(eng.stream(), None, 9, 0, S, y2, torch.zeros(3, dtype=torch.float64, device="cuda"))
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    assert whole.bit_errors > 0
