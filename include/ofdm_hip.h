@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define OFDM_ABI_VERSION 1
+#define OFDM_ABI_VERSION 2
 
 #define OFDM_OK 0
 #define OFDM_E_INVALID (-1)  /* bad argument / unsupported shape          */
@@ -45,6 +45,8 @@ enum ofdm_equalizer { OFDM_EQ_NONE = 0, OFDM_EQ_ZF = 1, OFDM_EQ_MMSE = 2 };
 
 /* prefix/models.py:29-113 (NoPrefixScheme = OFDM_PREFIX_CYCLIC with cp = 0) */
 enum ofdm_prefix { OFDM_PREFIX_CYCLIC = 0, OFDM_PREFIX_ZERO = 1 };
+/* modulation/models.py:19-91: OFDMModulator / SingleCarrierOFDMModulator */
+enum ofdm_modulator { OFDM_MOD_OFDM = 0, OFDM_MOD_SC = 1 };
 
 typedef struct ofdm_plan_s* ofdm_plan_t;
 
@@ -76,6 +78,8 @@ typedef struct ofdm_desc {
     /* Optional explicit equaliser response (IEqualizator(channel_frequency_response=H)),
        [n_fft] complex; overrides the response derived from h_raw. */
     const double* H;
+    /* enum ofdm_modulator (ABI 2): the fused path's modulator (ofdm_tx / ofdm_rx). */
+    int32_t modulator;
 } ofdm_desc;
 
 typedef struct ofdm_plan_info {
@@ -160,24 +164,29 @@ int ofdm_power(ofdm_plan_t plan, void* stream, const void* y, int64_t len, doubl
  *
  * Bit source: `bits` != NULL -> packed tx bytes of the WHOLE run (OFDM symbol s
  * starts at bit s*bits_per_ofdm_symbol), e.g. the reference's PCG64 bytes
- * (parity mode).  bits == NULL -> counter-based Philox4x32-10 bits keyed by
- * `seed`, counter (global symbol, word) (throughput mode).
+ * (parity mode).  bits == NULL -> throughput mode: bits and noise from the
+ * counter-based lane streams keyed by (seed, global symbol) (Philox4x32-10 seeding
+ * SFC32; definition in csrc/ofdm_device.hpp, restated in oracle/philox_streams.py).
  *
- * ofdm_tx: for global OFDM symbols [sym0, sym0+n_sym): map -> IFFT(ortho) -> cp
- *   -> linear convolution with the normalised CIR across symbol boundaries
- *   (channel/models.py:52-55).  Writes the N kept (post-prefix) channel-output
- *   samples of each symbol to y[(s-sym0)*N + n] (y may be NULL: power pass only)
- *   and accumulates into stats (device doubles): stats[0] += sum|y|^2 over all
- *   N+cp samples (noise/models.py:14), stats[1] += sum|x|^2, stats[2] = max(stats[2],
- *   max|x|^2) over the modulated samples incl. the prefix (simulation/models.py:519-522).
+ * ofdm_tx: for global OFDM symbols [sym0, sym0+n_sym): map -> IFFT(ortho) (OFDM) or
+ *   nothing (single carrier) -> cyclic prefix or zero guard -> linear convolution with
+ *   the normalised CIR across symbol boundaries (channel/models.py:52-55).  Writes the
+ *   channel-output samples of each symbol to y[(s-sym0)*ystride + n], ystride = N (the
+ *   post-prefix samples) or N + cp with zero padding (all samples: the receiver
+ *   overlap-adds the guard); y may be NULL (power pass only).  Accumulates into stats
+ *   (device doubles): stats[0] += sum|y|^2 over all N+cp samples (noise/models.py:14),
+ *   stats[1] += sum|x|^2, stats[2] = max(stats[2], max|x|^2) over the modulated samples
+ *   incl. the guard (simulation/models.py:519-522).
  *
  * ofdm_rx: adds AWGN with sigma^2 = (stats[0]/total_samples)/10^(snr/10) (noise_on=0:
- *   no noise), strips the prefix, FFT(ortho), equalises (MMSE noise variance per OFDM
- *   symbol, equalization/models.py:39-49), slices to the nearest constellation point
- *   and compares against the tx bits: counters[0] += bit errors over global bit
- *   positions < n_valid_bits, counters[1] += symbol errors (simulation/models.py:596-606).
+ *   no noise), strips the prefix (or overlap-adds the zero guard, prefix/models.py:69-101),
+ *   FFT(ortho), equalises (MMSE noise variance per OFDM symbol, equalization/models.py:
+ *   39-49), IFFT(ortho) for single carrier, decides the nearest constellation point
+ *   (per-axis slicer for square QAM, brute force over the LUT otherwise) and compares
+ *   against the tx bits: counters[0] += bit errors over global bit positions
+ *   < n_valid_bits, counters[1] += symbol errors (simulation/models.py:596-606).
  *   Noise: nr/ni != NULL -> the reference's normals for the whole serial stream
- *   (sample s*(N+cp)+m); NULL -> Philox4x32-10 + Box-Muller keyed by seed.
+ *   (sample s*(N+cp)+m); NULL -> the throughput-mode lane streams, Box-Muller.
  *   z_out (optional): the equalised symbols of the first z_keep OFDM symbols of this
  *   call, (z_keep, N) complex -- the results' received_symbols (simulation/models.py:618).
  */

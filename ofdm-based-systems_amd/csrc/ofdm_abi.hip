@@ -95,7 +95,7 @@ struct ofdm_plan_s {
     int adaptive, b, bps, n_axis, lut_len, n_active;
     double gain_mean;
     DevBuf tw, ptw, lut, lut64, h, eq_a, eq_b, axis, sc, active, ws, H64;
-    int has_const, has_channel, separable, zp;
+    int has_const, has_channel, separable, zp, single_carrier;
     size_t csize() const { return prec == OFDM_F32 ? 8 : 16; }
 };
 
@@ -213,6 +213,9 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
     if (d->prefix != OFDM_PREFIX_CYCLIC && d->prefix != OFDM_PREFIX_ZERO)
         return fail(OFDM_E_INVALID, "bad prefix kind");
     p->zp = d->prefix == OFDM_PREFIX_ZERO;
+    if (d->modulator != OFDM_MOD_OFDM && d->modulator != OFDM_MOD_SC) return fail(OFDM_E_INVALID, "bad modulator kind");
+    p->single_carrier = d->modulator == OFDM_MOD_SC;
+    if (p->zp && p->cp > p->n) return fail(OFDM_E_INVALID, "zero padding needs prefix length <= n_fft");
     p->adaptive = d->sc_lut != nullptr;
     p->has_const = d->n_luts > 0;
     p->has_channel = d->n_taps > 0 || d->H != nullptr;
@@ -594,13 +597,17 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
     c.gain_mean = p->gain_mean;
     c.eq_a = p->eq_a.p;
     c.eq_b = p->eq_b.p;
+    c.scm = p->single_carrier;
+    c.zpad = p->zp && p->cp > 0;
+    c.nn = !p->separable;
+    c.ystride = c.zpad ? p->n + p->cp : p->n;
+    c.lut64 = (const double*)p->lut64.p;
 }
 
 int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int64_t sym0, int64_t n_sym,
             void* y, double* stats) {
     if (!p || !p->has_const || p->L < 1) return fail(OFDM_E_INVALID, "ofdm_tx needs a constellation and channel taps");
-    if (!p->separable) return fail(OFDM_E_INVALID, "fused path needs square-QAM constellations");
-    if (p->zp) return fail(OFDM_E_INVALID, "fused path supports the cyclic prefix only");
+    if (!p->separable && p->adaptive) return fail(OFDM_E_INVALID, "adaptive loading needs square-QAM constellations");
     if (p->L - 1 > p->n) return fail(OFDM_E_INVALID, "fused path needs channel order <= n_fft");
     if (n_sym < 0 || sym0 < 0 || !stats) return fail(OFDM_E_INVALID, "bad argument to ofdm_tx");
     if (n_sym == 0) return OFDM_OK;
@@ -626,8 +633,7 @@ int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const 
             int64_t sym0, int64_t n_sym, int64_t n_valid_bits, uint64_t* counters, void* z_out,
             int64_t z_keep) {
     if (!p || !p->has_const) return fail(OFDM_E_INVALID, "ofdm_rx needs a constellation");
-    if (!p->separable) return fail(OFDM_E_INVALID, "fused path needs square-QAM constellations");
-    if (p->zp) return fail(OFDM_E_INVALID, "fused path supports the cyclic prefix only");
+    if (!p->separable && p->adaptive) return fail(OFDM_E_INVALID, "adaptive loading needs square-QAM constellations");
     if (p->eq != OFDM_EQ_NONE && !p->has_channel) return fail(OFDM_E_INVALID, "plan has no channel response");
     if (n_sym < 0 || sym0 < 0 || !counters || (n_sym > 0 && !y) || (noise_on && (!stats || total_samples <= 0)))
         return fail(OFDM_E_INVALID, "bad argument to ofdm_rx");

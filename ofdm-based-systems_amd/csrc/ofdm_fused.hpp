@@ -147,6 +147,11 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
     const TxRxCommon& cm = a.c;
     const bool adaptive = FB ? false : (bool)cm.adaptive;
+    // generic kernel variants: single-carrier OFDM (no IFFT, modulation/models.py:
+    // 58-70) and the zero-padding guard (prefix/models.py:55-67: [x | 0 ... 0])
+    const bool scm = FB ? false : (bool)cm.scm;
+    const bool zp = FB ? false : (bool)cm.zpad;
+    const int ystride = FB ? N : cm.ystride;  // stored samples per OFDM symbol: N, or N + cp (ZP)
     const int cp = cm.cp, L = a.L;
     const int slot = a.slot;  // complex elements per symbol row (>= PADN and >= L-1+cp+N)
     const int tls = L > 1 ? L - 1 : 1;
@@ -165,7 +170,8 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
     if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
     // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element)
-    for (int i = threadIdx.x; i < cm.lut_len; i += BLK) lut[i] = cscale(((const C*)cm.lut)[i], (R)cm.scale);
+    const R lut_scale = scm ? (R)1 : (R)cm.scale;
+    for (int i = threadIdx.x; i < cm.lut_len; i += BLK) lut[i] = cscale(((const C*)cm.lut)[i], lut_scale);
     if (threadIdx.x < L) h[threadIdx.x] = ((const C*)a.h)[threadIdx.x];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     __syncthreads();
@@ -212,7 +218,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
                     x[i] = v;
                 }
             }
-            if (!(a.flags & 2)) fft_reg<R, LOGN, true, (FB > 0)>(x, row, tw, tw + 64, t, tt);
+            if (!(a.flags & 2) && !scm) fft_reg<R, LOGN, true, (FB > 0)>(x, row, tw, tw + 64, t, tt);
             // The prefix repeats samples k >= N - cp.  With cp <= TPS only the lane's last
             // element can be one of them (one loop-invariant compare); otherwise the compares
             // are made per symbol against an opaque copy of N - cp, so they are not hoisted
@@ -220,6 +226,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
             int ncp = N - cp;
             asm volatile("" : "+s"(ncp));
             auto prefix_sum = [&](auto&& pw) -> R {
+                if (zp) return (R)0;  // the zero guard adds no power
                 if (cp <= TPS) return t >= TPS - cp ? pw(E - 1) : (R)0;
                 R acc = 0;
 #pragma unroll
@@ -244,12 +251,14 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
             if (L == 1) {
                 // flat channel: y = h0 x, no inter-symbol memory
                 if (active && c >= 0) {
-                    C* yo = yout + sl * N;
+                    C* yo = yout + sl * ystride;
 #pragma unroll
                     for (int i = 0; i < E; ++i) {
                         const C yv = cmul(h0, x[i]);
                         if (yout && !(a.flags & 4)) yo[t + i * TPS] = yv;
                     }
+                    if (zp && yout)
+                        for (int j = t; j < cp; j += TPS) yo[N + j] = mk<R>(0, 0);
                     if constexpr (FB > 0) {
                         py += (double)(norm2(h0) * pxs);  // |y|^2 = |h0|^2 |x|^2 (complex64 mode)
                     } else {
@@ -262,12 +271,15 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
                 }
                 sym_sync<TPS>();  // W / row reuse by the next symbol
             } else {
-                // extended serial stream in the row: [tail (L-1) | prefix (cp) | x (N)]
+                // extended serial stream in the row: [tail (L-1) | prefix (cp) | x (N)], or with
+                // zero padding [tail (L-1) | x (N) | zeros (cp)]
                 sym_sync<TPS>();  // the last FFT pass has read the row
-                const int o = L - 1 + cp;
+                const int o = zp ? L - 1 : L - 1 + cp;
 #pragma unroll
                 for (int i = 0; i < E; ++i) row[o + t + i * TPS] = x[i];
-                if (cp <= TPS) {
+                if (zp) {
+                    for (int j = t; j < cp; j += TPS) row[L - 1 + N + j] = mk<R>(0, 0);
+                } else if (cp <= TPS) {
                     if (t >= TPS - cp) row[L - 1 + t - (TPS - cp)] = x[E - 1];
                 } else {
 #pragma unroll
@@ -287,7 +299,12 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
 #pragma unroll 8
                         for (int l = 0; l < L; ++l) yv = yv + cmul(h[l], e[-l]);
                         pys += norm2(yv);
-                        if (yout && m >= cp && !(a.flags & 4)) yout[sl * N + (m - cp)] = yv;
+                        if (yout && !(a.flags & 4)) {
+                            if (zp)
+                                yout[sl * ystride + m] = yv;  // every stream sample (RX overlap-adds)
+                            else if (m >= cp)
+                                yout[sl * N + (m - cp)] = yv;
+                        }
                     }
                     py += pys;
                 }
@@ -319,6 +336,13 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     const TxRxCommon& cm = a.c;
     const int eq = EQ >= 0 ? EQ : cm.eq;
     const bool adaptive = FB ? false : (bool)cm.adaptive;
+    // generic kernel variants: single-carrier OFDM (FFT -> equalise -> IFFT,
+    // modulation/models.py:72-91), zero-padding guard (overlap-add, prefix/models.py:69-101)
+    // and non-separable constellations (PSK: brute-force nearest point, constellation/models.py:19-27)
+    const bool scm = FB ? false : (bool)cm.scm;
+    const bool zp = FB ? false : (bool)cm.zpad;
+    const bool nn = FB ? false : (bool)cm.nn;
+    const int ystride = FB ? N : cm.ystride;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
     AxisInfo* axis = cv.take<AxisInfo>(4);
@@ -368,7 +392,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
         TxBits<FB, TPS> tb;
         tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
         // kept channel samples + AWGN; the 1/sqrt(N) of fft(norm="ortho") folded in
-        const C* ys = (const C*)a.y + sl * N;
+        const C* ys = (const C*)a.y + sl * ystride;
         C x[E];
         if (active && !(a.flags & 16)) {
 #pragma unroll
@@ -377,16 +401,16 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
 #pragma unroll
             for (int i = 0; i < E; ++i) x[i] = mk<R>(0, 0);
         }
+        const float m2s2ln2 = -1.3862943611198906f * (float)sigma * (float)sigma;
         if (active && array_noise) {
-            const double* nr = a.nr + sg * (N + cp) + cp;
-            const double* ni = a.ni + sg * (N + cp) + cp;
+            const double* nr = a.nr + sg * (N + cp) + (zp ? 0 : cp);
+            const double* ni = a.ni + sg * (N + cp) + (zp ? 0 : cp);
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 x[i].re += sigma * (R)nr[t + i * TPS];
                 x[i].im += sigma * (R)ni[t + i * TPS];
             }
         } else if (active && noise) {
-            const float m2s2ln2 = -1.3862943611198906f * (float)sigma * (float)sigma;
             static_assert(E % 2 == 0 || E == 1, "noise pairs");
 #pragma unroll
             for (int i = 0; i + 1 < E; i += 2) {
@@ -405,6 +429,26 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                 x[0] = x[0] + mk<R>((R)n0.x, (R)n0.y);
             }
         }
+        if (zp && active) {
+            // zero guard: received sample N + k (k < cp) is added onto sample k, noise included
+            // (philox mode: one more lane draw per tail sample, after the elements' noise)
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                const int k = t + i * TPS;
+                if (k < cp) {
+                    C v = (a.flags & 16) ? mk<R>(0, 0) : ys[N + k];
+                    if (array_noise) {
+                        v.re += sigma * (R)a.nr[sg * (N + cp) + N + k];
+                        v.im += sigma * (R)a.ni[sg * (N + cp) + N + k];
+                    } else if (noise) {
+                        f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
+                        tb.g.add_noise2(n0, n1, m2s2ln2);
+                        v = v + mk<R>((R)n0.x, (R)n0.y);
+                    }
+                    x[i] = x[i] + v;
+                }
+            }
+        }
         if constexpr (FB == 0) {
 #pragma unroll
             for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
@@ -421,6 +465,21 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
             if constexpr (FB > 0) p *= scale * scale;  // power of the ortho-scaled spectrum
             nv = cm.gain_mean == 0.0 ? (R)INFINITY : ((p / (R)N) / (R)a.snr_lin) / (R)cm.gain_mean;
         }
+        if (scm) {
+            // single carrier: equalise every subcarrier, back to time with ifft(ortho)
+#pragma unroll
+            for (int i = 0; i < E; ++i) {
+                const int k = t + i * TPS;
+                if (eq == OFDM_EQ_ZF)
+                    x[i] = cmul(x[i], eqa[k]);
+                else if (eq == OFDM_EQ_MMSE)
+                    x[i] = cmul(x[i], mmse_coef<R>(eqa[k], eqb[k], nv));
+            }
+            sym_sync<TPS>();  // the forward FFT has read the row
+            fft_reg<R, LOGN, true, false>(x, row, tw, tw + 64, t, tt);
+#pragma unroll
+            for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
+        }
         if (active && !(a.flags & 8)) {
             const int64_t sbit = sg * cm.bps;
             const bool all_valid = FB > 0 || sbit + cm.bps <= a.n_valid_bits;
@@ -428,6 +487,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
             auto equalized = [&](int i) {
                 const int k = t + i * TPS;
                 C v = x[i];
+                if (scm) return v;  // single carrier: equalised before the IFFT below
                 if (eq == OFDM_EQ_ZF) {
                     v = cmul(v, eqa[k]);
                 } else if (eq == OFDM_EQ_MMSE) {
@@ -463,7 +523,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                     } else {
                         b = cm.b;
                         off = k * b;
-                        ridx = slicer(v);
+                        ridx = nn ? (uint32_t)nn_index((double)v.re, (double)v.im, cm.lut64, cm.lut_len) : slicer(v);
                     }
                     uint32_t d = ridx ^ tb.generic(i, b, off);
                     ses += d != 0u;

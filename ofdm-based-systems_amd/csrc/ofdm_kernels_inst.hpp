@@ -119,7 +119,7 @@ static hipError_t tx_launch(const TxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
-        if (!a.c.adaptive && a.c.bits == nullptr) {
+        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn) {
             switch (a.c.b) {
                 case 2: return tx_launch<R, LOGN, 2>(a, grid, s);
                 case 4: return tx_launch<R, LOGN, 4>(a, grid, s);
@@ -170,7 +170,8 @@ static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN>
 static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
-        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr) {
+        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr && !a.c.scm &&
+            !a.c.zpad && !a.c.nn) {
             switch (a.c.b) {
                 case 2: return rx_eq<R, LOGN, 2>(a, grid, s);
                 case 4: return rx_eq<R, LOGN, 4>(a, grid, s);

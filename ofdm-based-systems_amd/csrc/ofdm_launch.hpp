@@ -98,6 +98,11 @@ struct TxRxCommon {
     double scale, gain_mean;
     const void* eq_a;
     const void* eq_b;
+    // generic-kernel variants: single-carrier OFDM, zero-padding guard,
+    // nearest-point decisions over the double LUT for non-separable constellations (PSK)
+    int scm, zpad, nn;
+    int ystride;  // stored channel samples per OFDM symbol: N, or N + cp with zero padding
+    const double* lut64;
 };
 
 struct TxArgs {

@@ -24,11 +24,12 @@ import torch
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
                          "libofdm_hip%s.so" % ("_" + os.environ["OFDM_LIB_VARIANT"]
                                                if os.environ.get("OFDM_LIB_VARIANT") else ""))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OFDM_F32, OFDM_F64 = 0, 1
 EQ_NONE, EQ_ZF, EQ_MMSE = 0, 1, 2
 PREFIX_CYCLIC, PREFIX_ZERO = 0, 1
+MOD_OFDM, MOD_SC = 0, 1
 
 _c_i32p = ctypes.POINTER(ctypes.c_int32)
 _c_f64p = ctypes.POINTER(ctypes.c_double)
@@ -56,6 +57,7 @@ class Desc(ctypes.Structure):
         ("n_taps", ctypes.c_int32),
         ("h_raw", _c_f64p),
         ("H", _c_f64p),
+        ("modulator", ctypes.c_int32),
     ]
 
 
@@ -178,7 +180,7 @@ class Plan:
     def __init__(self, n_fft: int, cp: int = 0, precision: int = OFDM_F64, equalizer: int = EQ_NONE,
                  luts: Optional[list] = None, sc_lut: Optional[np.ndarray] = None,
                  h_raw: Optional[np.ndarray] = None, H: Optional[np.ndarray] = None,
-                 prefix: int = PREFIX_CYCLIC):
+                 prefix: int = PREFIX_CYCLIC, modulator: int = MOD_OFDM):
         self._lib = lib()
         self._handle = ctypes.c_void_p()
         luts = luts or []
@@ -193,6 +195,7 @@ class Plan:
         d.n_fft = int(n_fft)
         d.cp = int(cp)
         d.prefix = int(prefix)
+        d.modulator = int(modulator)
         d.precision = int(precision)
         d.equalizer = int(equalizer)
         d.n_luts = len(luts)

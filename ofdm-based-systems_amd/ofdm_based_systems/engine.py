@@ -61,11 +61,19 @@ def shard(n: int, rank: int, world: int) -> tuple:
 
 class LinkEngine:
     def __init__(self, n_fft: int, cp: int, h_raw: np.ndarray, equalizer: int, luts: Sequence[np.ndarray],
-                 sc_lut: Optional[np.ndarray] = None, precision: int = B.OFDM_F64):
+                 sc_lut: Optional[np.ndarray] = None, precision: int = B.OFDM_F64,
+                 prefix: int = B.PREFIX_CYCLIC, modulator: int = B.MOD_OFDM):
+        """prefix: cyclic prefix (or none, cp = 0) or zero padding; modulator: OFDM or
+        single-carrier OFDM; non-square constellations (PSK) are decided by
+        brute-force nearest point."""
         self.plan = B.Plan(n_fft=n_fft, cp=cp, precision=precision, equalizer=equalizer, luts=list(luts),
-                           sc_lut=sc_lut, h_raw=np.asarray(h_raw, np.complex128))
+                           sc_lut=sc_lut, h_raw=np.asarray(h_raw, np.complex128), prefix=prefix,
+                           modulator=modulator)
         self.n_fft = n_fft
         self.cp = cp
+        # stored channel samples per OFDM symbol: the post-prefix N, or all N + cp with
+        # zero padding (the receiver overlap-adds the guard)
+        self.ystride = n_fft + cp if prefix == B.PREFIX_ZERO else n_fft
         self.bps = self.plan.bits_per_ofdm_symbol
         self.adaptive = self.plan.adaptive
         self.cdtype = self.plan.cdtype
@@ -155,7 +163,7 @@ class LinkEngine:
         stats = torch.zeros(3, dtype=torch.float64, device=dev)
         counters = torch.zeros(2, dtype=torch.int64, device=dev)
         csize = 8 if self.cdtype == torch.complex64 else 16
-        per_batch = batch or max(1, min(mine, y_budget // (N * csize)))
+        per_batch = batch or max(1, min(mine, y_budget // (self.ystride * csize)))
         keep = min(keep_symbols, mine)
         z_out = torch.empty((keep, N), dtype=self.cdtype, device=dev) if keep else None
 
@@ -172,7 +180,7 @@ class LinkEngine:
 
         if per_batch >= mine:
             # whole shard resident: one TX, one RX
-            y = torch.empty((max(mine, 1), N), dtype=self.cdtype, device=dev)
+            y = torch.empty((max(mine, 1), self.ystride), dtype=self.cdtype, device=dev)
             self._timed(events, "ofdm_tx", mine, lambda: self.tx(stream, bits_d, seed, lo, mine, y, stats))
             reduce_stats()
             self._timed(events, "ofdm_rx", mine, lambda: self.rx(
@@ -183,7 +191,7 @@ class LinkEngine:
             self.tx(stream, bits_d, seed, lo, mine, None, stats)
             reduce_stats()
             scratch = torch.zeros(3, dtype=torch.float64, device=dev)
-            y = torch.empty((per_batch, N), dtype=self.cdtype, device=dev)
+            y = torch.empty((per_batch, self.ystride), dtype=self.cdtype, device=dev)
             for b0 in range(lo, hi, per_batch):
                 nb = min(per_batch, hi - b0)
                 self.tx(stream, bits_d, seed, b0, nb, y, scratch)

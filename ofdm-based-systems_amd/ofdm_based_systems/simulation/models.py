@@ -348,15 +348,25 @@ class Simulation:
         # ---------------- data path
         reference = self.rng_mode == "reference"
         tx_bytes = _stream_bytes(bits_gen.generate_bits(total_bits)) if reference else None
-        fused = (self.modulator_type == ModulationType.OFDM and self.prefix_scheme != PrefixType.ZERO
-                 and self.constellation_scheme == ConstellationType.QAM)
+        # every built-in strategy runs on the fused kernels (SC-OFDM, zero padding and PSK on
+        # the generic kernel); a user-supplied strategy class falls back to the composed
+        # GPU operators, which call its own methods
+        mod_cls = self.MODULATOR_SCHEME_MAPPERS.get(self.modulator_type, OFDMModulator)
+        pre_cls = self.PREFIX_SCHEME_MAPPERS.get(self.prefix_scheme, NoPrefixScheme)
+        fused = (mod_cls in (OFDMModulator, SingleCarrierOFDMModulator)
+                 and pre_cls in (CyclicPrefixScheme, ZeroPaddingPrefixScheme, NoPrefixScheme)
+                 and type(mapper) in (QAMConstellationMapper, PSKConstellationMapper, AdaptiveConstellationMapper)
+                 and not (adaptive and self.modulator_type == ModulationType.SC_OFDM)
+                 and len(h_raw) - 1 <= N and cp <= N)
         if not fused and not reference:
-            raise ValueError("rng_mode='philox' needs OFDM with a cyclic/no prefix and QAM")
+            raise ValueError("rng_mode='philox' needs the built-in modulators, prefixes and constellations")
         t0 = time.perf_counter()
         if fused:
             luts, sc = (mapper.lut_tables() if adaptive else ([mapper.constellation], None))
             prec = B.OFDM_F32 if self.precision == "f32" else B.OFDM_F64
-            engine = LinkEngine(N, cp, h_raw, _EQ_KIND[self.equalizator_type], luts, sc, prec)
+            engine = LinkEngine(N, cp, h_raw, _EQ_KIND[self.equalizator_type], luts, sc, prec,
+                                prefix=B.PREFIX_ZERO if pre_cls is ZeroPaddingPrefixScheme else B.PREFIX_CYCLIC,
+                                modulator=B.MOD_SC if mod_cls is SingleCarrierOFDMModulator else B.MOD_OFDM)
             noise_on = isinstance(noise_model, AWGNoiseModel)
             normals = None
             if reference and noise_on:

@@ -134,31 +134,70 @@ class PhiloxLink:
     x_power_sum: float
     x_peak: float
     idx: np.ndarray        # (S, N) tx constellation indices
-    y: np.ndarray          # (S, N) kept channel samples (before noise)
+    y: np.ndarray          # stored channel samples before noise: (S, N) kept, or (S, N+cp) with ZP
 
 
 def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq: str, snr_db: float,
-               noise_on: bool = True) -> PhiloxLink:
-    """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic."""
+               noise_on: bool = True, modulator: str = "OFDM", prefix: str = "CP",
+               scheme: str = "QAM") -> PhiloxLink:
+    """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic.
+
+    modulator "OFDM" | "SC" (modulation/models.py:58-91), prefix "CP" | "ZP"
+    (prefix/models.py:29-101), scheme "QAM" | "PSK".  With zero padding every lane draws,
+    after its elements' noise, one more noise triple per received tail sample
+    N + k (k = t + i*TPS < cp, in order of i) and uses its first sample.
+    """
     b = int(np.log2(M))
-    lut = O.qam_lut(M)
+    lut = O.qam_lut(M) if scheme == "QAM" else O.psk_lut(M)
+    E, tps = geometry(N)
     gen = lane_generators(seed, np.arange(S), N)
     idx = tx_indices(gen, S, N, b)
-    x = O.modulate(lut[idx], cp)                       # (S, N+cp) incl. prefix
+    X = lut[idx]
+    s_t = np.fft.ifft(X, axis=1, norm="ortho") if modulator == "OFDM" else X
+    if prefix == "ZP":
+        x = np.concatenate([s_t, np.zeros((S, cp), np.complex128)], axis=1)
+    else:
+        x = O.add_cp(s_t, cp)                          # (S, N+cp) incl. prefix
     px = float(np.sum(np.abs(x) ** 2))
     mx = float(np.max(np.abs(x) ** 2))
-    y = O.channel_conv(x.ravel(), np.asarray(h_raw, np.complex128))
+    y = O.channel_conv(x.ravel(), np.asarray(h_raw, np.complex128)).reshape(S, N + cp)
     py = float(np.sum(np.abs(y) ** 2))
-    yk = y.reshape(S, N + cp)[:, cp:]
+    if prefix == "ZP":
+        yk, tail = y[:, :N].copy(), y[:, N:].copy()
+    else:
+        yk, tail = y[:, cp:].copy(), None
     rxs = yk.copy()
     if noise_on:
         p = py / (S * (N + cp))
         sigma = np.sqrt((p / 10 ** (snr_db / 10)) / 2.0)
         rxs = rxs + lane_noise(gen, S, N, sigma)
+    if prefix == "ZP" and cp > 0:
+        if noise_on:
+            t = np.tile(np.arange(tps), S)
+            for i in range(E):
+                k = t + i * tps
+                n = lane_noise_tail(gen, sigma)
+                use = k < cp
+                srow = np.repeat(np.arange(S), tps)[use]
+                tail[srow, k[use]] += n[use]
+        rxs[:, :cp] += tail
     H = np.fft.fft(np.asarray(h_raw, np.complex128), N)
     Z = O.equalize(np.fft.fft(rxs, axis=1, norm="ortho"), H, eq, snr_db)
+    if modulator == "SC":
+        Z = np.fft.ifft(Z, axis=1, norm="ortho")
     ridx = O.nn_demap(Z.ravel(), lut).reshape(S, N)
     diff = (ridx ^ idx).astype(np.uint64)
     be = int(sum(int(np.count_nonzero((diff >> np.uint64(j)) & np.uint64(1))) for j in range(b)))
     se = int(np.count_nonzero(ridx != idx))
-    return PhiloxLink(be, se, py, px, mx, idx, yk)
+    return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk)
+
+
+def lane_noise_tail(gen: Sfc32, sigma: float) -> np.ndarray:
+    """One noise triple per lane (all lanes draw; only lanes owning a tail sample use it)."""
+    sig = np.float32(sigma)
+    m2s2ln2 = np.float32(-1.3862943611198906) * sig * sig
+    u = [gen.next(), gen.next()]
+    a = gen.next()
+    uf = (u[0].astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -32)
+    r = np.sqrt(np.float64(m2s2ln2) * np.log2(uf.astype(np.float64)))
+    return r * np.exp(2j * np.pi * (a >> np.uint32(16)).astype(np.float64) * 2.0 ** -16)

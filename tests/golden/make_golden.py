@@ -324,6 +324,35 @@ def runs() -> list:
     add("next_psk8_n64_p1_mmse", 1, "Lin-Phoong_P1", num_symbols=64 * 100, num_subcarriers=64,
         constellation_order=8, prefix_scheme=CP, prefix_length_ratio=1.0, equalizator_type=MM,
         snr_db=18.0, **dict(base, constellation_scheme=ConstellationType.PSK))
+    # SURVEY 8(f) rows on the fused path: published ZP rows (docs tex:257-260), SC-OFDM, PSK
+    for ratio in (0.34, 1.0):
+        add(f"published_zp{ratio:.2f}_mmse", 1, "Lin-Phoong_P2", num_bits=6_000_000,
+            num_subcarriers=64, constellation_order=64, prefix_scheme=ZP, prefix_length_ratio=ratio,
+            equalizator_type=MM, snr_db=30.0, **base)
+    add("next_zp_n256_m64_severe_zf", 2, "severe_multipath", num_symbols=256 * 40, num_subcarriers=256,
+        constellation_order=64, prefix_scheme=ZP, prefix_length_ratio=1.0, equalizator_type=ZF,
+        snr_db=28.0, **base)
+    add("next_zp_n128_m16_severe_cp050_mmse", 3, "severe_multipath", num_symbols=128 * 40,
+        num_subcarriers=128, constellation_order=16, prefix_scheme=ZP, prefix_length_ratio=0.5,
+        equalizator_type=MM, snr_db=24.0, **base)
+    add("next_scofdm_n256_m16_severe_mmse", 2, "severe_multipath", num_symbols=256 * 40,
+        num_subcarriers=256, constellation_order=16, prefix_scheme=CP, prefix_length_ratio=1.0,
+        equalizator_type=MM, snr_db=22.0, **dict(base, modulator_type=ModulationType.SC_OFDM))
+    add("next_scofdm_zp_n64_qpsk_p2_zf", 3, "Lin-Phoong_P2", num_symbols=64 * 60, num_subcarriers=64,
+        constellation_order=4, prefix_scheme=ZP, prefix_length_ratio=1.0, equalizator_type=ZF,
+        snr_db=15.0, **dict(base, modulator_type=ModulationType.SC_OFDM))
+    add("next_scofdm_n128_m64_flat_none", 4, "flat_fading", num_symbols=128 * 40, num_subcarriers=128,
+        constellation_order=64, prefix_scheme=CP, prefix_length_ratio=1.0, equalizator_type=NE,
+        snr_db=20.0, **dict(base, modulator_type=ModulationType.SC_OFDM))
+    for m, ch, eq, snr, ratio in ((2, "severe_multipath", ZF, 8.0, 1.0), (4, "flat_fading", NE, 6.0, 1.0),
+                                  (16, "Lin-Phoong_P1", MM, 22.0, 1.0), (8, "severe_multipath", MM, 20.0, 0.5)):
+        add(f"next_psk{m}_n128_{ch}_r{ratio:.1f}", 2, ch, num_symbols=128 * 40, num_subcarriers=128,
+            constellation_order=m, prefix_scheme=CP, prefix_length_ratio=ratio, equalizator_type=eq,
+            snr_db=snr, **dict(base, constellation_scheme=ConstellationType.PSK))
+    add("next_psk8_zp_scofdm_n64_p1_mmse", 5, "Lin-Phoong_P1", num_symbols=64 * 60, num_subcarriers=64,
+        constellation_order=8, prefix_scheme=ZP, prefix_length_ratio=1.0, equalizator_type=MM,
+        snr_db=16.0, **dict(base, constellation_scheme=ConstellationType.PSK,
+                            modulator_type=ModulationType.SC_OFDM))
     return cases
 
 

@@ -26,6 +26,7 @@ class OracleEngine(LinkEngine):
 
     def __init__(self, N, M, h_raw, cp, eq):
         self.n_fft, self.cp, self.h, self.eq = N, cp, np.asarray(h_raw, np.complex128), eq
+        self.ystride = N  # cyclic prefix: the kept samples
         self.b = int(np.log2(M))
         self.bps = N * self.b
         self.adaptive = False

@@ -31,38 +31,57 @@ pytestmark = pytest.mark.gpu
 
 EQ = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}
 
-# N, M, channel, equaliser, OFDM symbols, SNR dB (BER ~1e-3 .. 1e-2), precision
+# N, M, channel, equaliser, OFDM symbols, SNR dB (BER ~1e-3 .. 1e-2), precision, variant
 CASES = [
-    (1024, 64, "flat_fading", "NONE", 512, 20.0, B.OFDM_F32),
-    (1024, 64, "severe_multipath", "MMSE", 512, 24.0, B.OFDM_F32),
-    (256, 16, "Lin-Phoong_P1", "ZF", 1024, 22.0, B.OFDM_F32),
-    (64, 4, "rayleigh_fading", "ZF", 4096, 14.0, B.OFDM_F32),
-    (4096, 256, "Lin-Phoong_P1", "MMSE", 96, 31.0, B.OFDM_F32),
-    (2048, 16, "flat_fading", "NONE", 256, 14.0, B.OFDM_F32),
-    (32, 16, "flat_fading", "NONE", 8192, 14.0, B.OFDM_F32),
-    (1024, 64, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F64),
+    (1024, 64, "flat_fading", "NONE", 512, 20.0, B.OFDM_F32, {}),
+    (1024, 64, "severe_multipath", "MMSE", 512, 24.0, B.OFDM_F32, {}),
+    (256, 16, "Lin-Phoong_P1", "ZF", 1024, 22.0, B.OFDM_F32, {}),
+    (64, 4, "rayleigh_fading", "ZF", 4096, 14.0, B.OFDM_F32, {}),
+    (4096, 256, "Lin-Phoong_P1", "MMSE", 96, 31.0, B.OFDM_F32, {}),
+    (2048, 16, "flat_fading", "NONE", 256, 14.0, B.OFDM_F32, {}),
+    (32, 16, "flat_fading", "NONE", 8192, 14.0, B.OFDM_F32, {}),
+    (1024, 64, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F64, {}),
+    # SURVEY 8(f) variants on the generic kernel
+    (64, 4, "Lin-Phoong_P2", "ZF", 2048, 20.0, B.OFDM_F32, {"modulator": "SC"}),
+    (1024, 16, "severe_multipath", "MMSE", 256, 21.0, B.OFDM_F32, {"prefix": "ZP"}),
+    (256, 8, "Lin-Phoong_P1", "MMSE", 512, 17.0, B.OFDM_F32, {"scheme": "PSK"}),
+    (128, 4, "Lin-Phoong_P2", "MMSE", 1024, 10.0, B.OFDM_F64, {"modulator": "SC", "prefix": "ZP", "scheme": "PSK"}),
+    (2048, 16, "Lin-Phoong_P1", "MMSE", 128, 19.0, B.OFDM_F32, {"prefix": "ZP", "modulator": "SC"}),
 ]
-IDS = [f"N{c[0]}-M{c[1]}-{c[2]}-{c[3]}-{'f32' if c[6] == B.OFDM_F32 else 'f64'}" for c in CASES]
 
 
-def setup(N, M, ch, eq, prec):
+def _id(c):
+    v = "".join(f"-{k}={w}" for k, w in c[7].items())
+    return f"N{c[0]}-M{c[1]}-{c[2]}-{c[3]}-{'f32' if c[6] == B.OFDM_F32 else 'f64'}{v}"
+
+
+IDS = [_id(c) for c in CASES]
+
+
+def setup(N, M, ch, eq, prec, var=None):
+    var = var or {}
     h = channel(ch)
     cp = len(h) - 1
-    return LinkEngine(N, cp, h, EQ[eq], [O.qam_lut(M)], None, prec), h, cp
+    lut = O.psk_lut(M) if var.get("scheme") == "PSK" else O.qam_lut(M)
+    eng = LinkEngine(N, cp, h, EQ[eq], [lut], None, prec,
+                     prefix=B.PREFIX_ZERO if var.get("prefix") == "ZP" else B.PREFIX_CYCLIC,
+                     modulator=B.MOD_SC if var.get("modulator") == "SC" else B.MOD_OFDM)
+    return eng, h, cp
 
 
-@pytest.mark.parametrize("N,M,ch,eq,S,snr,prec", CASES, ids=IDS)
-def test_tx_samples_match_oracle(gpu, N, M, ch, eq, S, snr, prec):
-    eng, h, cp = setup(N, M, ch, eq, prec)
+@pytest.mark.parametrize("N,M,ch,eq,S,snr,prec,var", CASES, ids=IDS)
+def test_tx_samples_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
+    eng, h, cp = setup(N, M, ch, eq, prec, var)
     seed = 1234
-    y = torch.empty((S, N), dtype=eng.cdtype, device="cuda")
+    y = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
     stats = torch.zeros(3, dtype=torch.float64, device="cuda")
     eng.tx(eng.stream(), None, seed, 0, S, y, stats)
     torch.cuda.synchronize()
-    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, noise_on=False)
+    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, noise_on=False, **var)
     got = y.cpu().numpy()
     rms = np.sqrt(np.mean(np.abs(ref.y) ** 2))
     tol = 1e-4 if prec == B.OFDM_F32 else 1e-12
+    assert got.shape == ref.y.shape
     assert np.max(np.abs(got - ref.y)) <= tol * rms
     st = stats.cpu().numpy()
     rt = 1e-5 if prec == B.OFDM_F32 else 1e-12
@@ -71,12 +90,12 @@ def test_tx_samples_match_oracle(gpu, N, M, ch, eq, S, snr, prec):
     assert st[2] == pytest.approx(ref.x_peak, rel=rt)
 
 
-@pytest.mark.parametrize("N,M,ch,eq,S,snr,prec", CASES, ids=IDS)
-def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec):
-    eng, h, cp = setup(N, M, ch, eq, prec)
+@pytest.mark.parametrize("N,M,ch,eq,S,snr,prec,var", CASES, ids=IDS)
+def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
+    eng, h, cp = setup(N, M, ch, eq, prec, var)
     seed = 77
     res = eng.run(S, snr, seed=seed)
-    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr)
+    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, **var)
     assert ref.bit_errors > 100, "SNR too high for a meaningful count"
     for got, want in ((res.bit_errors, ref.bit_errors), (res.symbol_errors, ref.symbol_errors)):
         assert abs(got - want) <= 3 + 1e-3 * want, (got, want)

@@ -1,0 +1,84 @@
+"""Throughput of the fused path per modem variant (SURVEY 8(a) configs and the 8(f) rows).
+
+Times ofdm_tx / ofdm_rx with HIP events on the launch stream, throughput mode (complex64,
+bits and noise generated in the kernels), one GPU:
+
+    python tools/bench_variants.py [--symbols 200000] [--steps 5] > gpurun_out/variants.json
+
+Prints one JSON object per variant and a summary table on stderr.  Which kernel runs:
+OFDM + cyclic prefix + square QAM -> the throughput specialisation; SC-OFDM, zero
+padding and PSK -> the generic kernel.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ofdm-based-systems_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from ofdm_based_systems import _backend as B  # noqa: E402
+from ofdm_based_systems.constellation.models import PSKConstellationMapper, QAMConstellationMapper  # noqa: E402
+from ofdm_based_systems.engine import LinkEngine  # noqa: E402
+
+EQ = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}
+
+# name, N, M, scheme, channel, eq, snr, modulator, prefix
+VARIANTS = [
+    ("b: OFDM CP 64-QAM flat", 1024, 64, "QAM", "flat_fading", "NONE", 24.0, "OFDM", "CP"),
+    ("c: OFDM CP 64-QAM severe MMSE", 1024, 64, "QAM", "severe_multipath", "MMSE", 27.75, "OFDM", "CP"),
+    ("e: OFDM CP 256-QAM N=4096 P1 MMSE", 4096, 256, "QAM", "Lin-Phoong_P1", "MMSE", 30.0, "OFDM", "CP"),
+    ("f1: SC-OFDM CP 64-QAM severe MMSE", 1024, 64, "QAM", "severe_multipath", "MMSE", 27.75, "SC", "CP"),
+    ("f2: OFDM ZP 64-QAM severe MMSE", 1024, 64, "QAM", "severe_multipath", "MMSE", 27.75, "OFDM", "ZP"),
+    ("f3: OFDM CP 16-PSK severe MMSE", 1024, 16, "PSK", "severe_multipath", "MMSE", 27.75, "OFDM", "CP"),
+    ("f1+f2+f3: SC-OFDM ZP 8-PSK P2 ZF", 1024, 8, "PSK", "Lin-Phoong_P2", "ZF", 20.0, "SC", "ZP"),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--symbols", type=int, default=200_000)
+    ap.add_argument("--steps", type=int, default=5)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    rows = []
+    for name, N, M, scheme, ch, eq, snr, mod, pre in VARIANTS:
+        h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+        cp = len(h) - 1
+        lut = (QAMConstellationMapper(M) if scheme == "QAM" else PSKConstellationMapper(M)).constellation
+        eng = LinkEngine(N, cp, h, EQ[eq], [lut], None, B.OFDM_F32,
+                         prefix=B.PREFIX_ZERO if pre == "ZP" else B.PREFIX_CYCLIC,
+                         modulator=B.MOD_SC if mod == "SC" else B.MOD_OFDM)
+        S = args.symbols if N <= 1024 else args.symbols // (N // 1024)
+        eng.run(S, snr, seed=99)  # warm-up (plan, allocator, clocks)
+        torch.cuda.synchronize()
+        ev = []
+        t0 = time.perf_counter()
+        pend = [eng.run_async(S, snr, seed=k, events=ev) for k in range(args.steps)]
+        bits = sum(p.result().bit_errors for p in pend)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        ms = {}
+        for kname, n, e0, e1 in ev:
+            ms.setdefault(kname, []).append(e0.elapsed_time(e1))
+        row = {"variant": name, "n_fft": N, "order": M, "scheme": scheme, "modulator": mod, "prefix": pre,
+               "channel": ch, "equalizer": eq, "snr_db": snr, "symbols_per_step": S,
+               "ofdm_symbols_per_s": S / dt,
+               "ms_per_1e6_symbols": {k: float(np.mean(v)) * 1e6 / S for k, v in ms.items()},
+               "ber": bits / (args.steps * S * N * np.log2(M))}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    for r in rows:
+        k = r["ms_per_1e6_symbols"]
+        print(f"{r['variant']:38s} {r['ofdm_symbols_per_s']:10.3e} sym/s   tx {k['ofdm_tx']:6.2f}  rx {k['ofdm_rx']:6.2f}"
+              f" ms/1e6   BER {r['ber']:.2e}", file=sys.stderr)
+
+
+if __name__ == "__main__":
+    main()
