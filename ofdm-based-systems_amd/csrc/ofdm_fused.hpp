@@ -38,8 +38,18 @@
 
 namespace ofdm {
 
-template <int FB, int LOGN>
-constexpr int tx_block() { return FB > 0 && LOGN <= 10 ? OFDM_TX_FAST_BLOCK : kBlock; }
+// MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
+#ifndef OFDM_TX_MP_BLOCK
+#define OFDM_TX_MP_BLOCK 256
+#endif
+// LT (throughput TX): 0 flat channel; 4 / 8 multipath with <= LT taps through the register
+// window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps)
+template <int FB, int LOGN, int LT>
+constexpr int tx_block() {
+    return FB > 0 && LOGN <= 10 ? (LT != 0 ? OFDM_TX_MP_BLOCK : OFDM_TX_FAST_BLOCK) : kBlock;
+}
+// padded FIR row index of the throughput multipath TX: one slot per 16 elements
+__host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
 template <int FB, int LOGN, int EQ>
 constexpr int rx_block() { return FB > 0 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock; }
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
@@ -126,6 +136,29 @@ struct TxBits {
     }
 };
 
+// Nearest constellation point of a non-separable LUT (PSK).  complex128: the reference's
+// |z - C_m| with hypot and the first index on ties (nn_index); complex64 (throughput
+// mode): squared distances in float against the plan-precision LUT.
+template <typename R>
+__device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm) {
+    if constexpr (sizeof(R) == 8) {
+        return (uint32_t)nn_index(v.re, v.im, cm.lut64, cm.lut_len);
+    } else {
+        const cpx<float>* L = (const cpx<float>*)cm.lut;
+        float bd = INFINITY;
+        uint32_t best = 0;
+        for (int m = 0; m < cm.lut_len; ++m) {
+            const float dr = v.re - L[m].re, di = v.im - L[m].im;
+            const float d = dr * dr + di * di;
+            if (d < bd) {
+                bd = d;
+                best = (uint32_t)m;
+            }
+        }
+        return best;
+    }
+}
+
 template <int I, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
     if constexpr (I < E) {
@@ -138,10 +171,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 // Each symbol group walks `chunk` consecutive OFDM symbols so the FIR tail (last L-1
 // stream samples of the previous symbol) is carried in LDS; the first symbol of a chunk
 // regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
-template <typename R, int LOGN, int FB>
-__global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, LOGN>(), OFDM_TX_WAVES))) void k_tx(
+template <typename R, int LOGN, int FB, int LT>
+__global__ __launch_bounds__((tx_block<FB, LOGN, LT>()), (block_waves(tx_block<FB, LOGN, LT>(), OFDM_TX_WAVES))) void k_tx(
     TxArgs a) {
-    constexpr int BLK = tx_block<FB, LOGN>();
+    constexpr int BLK = tx_block<FB, LOGN, LT>();
+    constexpr bool WFIR = FB > 0 && LT > 0;  // register window FIR
     using G = Geo<LOGN, BLK>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
@@ -152,13 +186,14 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
     const bool scm = FB ? false : (bool)cm.scm;
     const bool zp = FB ? false : (bool)cm.zpad;
     const int ystride = FB ? N : cm.ystride;  // stored samples per OFDM symbol: N, or N + cp (ZP)
-    const int cp = cm.cp, L = a.L;
+    const int cp = cm.cp, L = LT != 0 ? a.L : 1;
     const int slot = a.slot;  // complex elements per symbol row (>= PADN and >= L-1+cp+N)
     const int tls = L > 1 ? L - 1 : 1;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
     C* lut = cv.take<C>(cm.lut_len);
     C* h = cv.take<C>(32);
+    C* hsw = cv.take<C>(WFIR ? 32 : 0);  // window FIR: the taps swizzled, (-im, re)
     AxisInfo* axis = cv.take<AxisInfo>(4);
     C* rows = cv.take<C>((size_t)G::SPB * slot);
     C* tails = cv.take<C>((size_t)G::SPB * tls);
@@ -172,7 +207,11 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
     // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element)
     const R lut_scale = scm ? (R)1 : (R)cm.scale;
     for (int i = threadIdx.x; i < cm.lut_len; i += BLK) lut[i] = cscale(((const C*)cm.lut)[i], lut_scale);
-    if (threadIdx.x < L) h[threadIdx.x] = ((const C*)a.h)[threadIdx.x];
+    if (threadIdx.x < 32) {
+        const C hq = threadIdx.x < L ? ((const C*)a.h)[threadIdx.x] : mk<R>(0, 0);
+        h[threadIdx.x] = hq;
+        if (WFIR) hsw[threadIdx.x] = mk<R>(-hq.im, hq.re);
+    }
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     __syncthreads();
 
@@ -183,6 +222,11 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
     uint32_t* W = words + ls * cm.words_per_sym;
     C* yout = (C*)a.y;
     const C h0 = h[0];
+    // window FIR: the stream sample m in [-(LT-1), N+cp) lives at row[fir_pad(R0 + m)], R0 chosen
+    // so that lane t's window (samples cp + 16 t - (LT-1) ..) starts at row index A + 16 t,
+    // A = 16 ceil(cp/16)
+    constexpr int LTN = WFIR ? LT : 1;
+    const int A = (cp + 15) & ~15, R0 = A - cp + LTN - 1;
     const int64_t ngroups = (cm.n_sym + a.chunk - 1) / a.chunk;
     const int64_t niter = (ngroups + G::SPB - 1) / G::SPB;
     double py = 0, px = 0, mx = 0;
@@ -270,6 +314,72 @@ __global__ __launch_bounds__((tx_block<FB, LOGN>()), (block_waves(tx_block<FB, L
                     }
                 }
                 sym_sync<TPS>();  // W / row reuse by the next symbol
+            } else if constexpr (WFIR) {
+                // throughput multipath (L <= LT, cp <= TPS, E = 16, TPS >= 16): lane t computes the
+                // 16 consecutive kept samples k = 16 t + j from a register window of 16 + LT - 1
+                // stream samples read once from LDS (fir_pad: lane stride 17 elements, conflict
+                // free; offsets compile-time) -- 23 LDS reads instead of 2 L per output
+                static_assert(E == 16 && TPS >= 16, "window FIR geometry");
+                constexpr int WN = E + LT - 1;
+                sym_sync<TPS>();  // the last FFT pass has read the row
+                {
+                    const int u = R0 + cp + t;  // stream sample cp + t + TPS i at fir_pad(u + TPS i)
+                    const int bx = fir_pad(u);
+#pragma unroll
+                    for (int i = 0; i < E; ++i) row[bx + TPS * i + (TPS * i >> 4)] = x[i];  // TPS i = 0 mod 16
+                }
+                if (t >= TPS - cp) row[fir_pad(R0 + t - (TPS - cp))] = x[E - 1];  // cyclic prefix
+                if (t < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
+                    const int z = t - (LT - L);
+                    row[fir_pad(R0 - (LT - 1) + t)] = z < 0 ? mk<R>(0, 0) : tl[z];
+                }
+                sym_sync<TPS>();
+                if (active && c >= 0) {
+                    f32x2 hv[LT], hs[LT];  // taps (zero past L), LDS broadcast reads
+#pragma unroll
+                    for (int q = 0; q < LT; ++q) {
+                        hv[q] = f32x2{(float)h[q].re, (float)h[q].im};
+                        hs[q] = f32x2{(float)hsw[q].re, (float)hsw[q].im};
+                    }
+                    const C* wb = row + (A + (A >> 4) + 17 * t);
+                    f32x2 win[WN];
+#pragma unroll
+                    for (int w = 0; w < WN; ++w) {
+                        const C ev = wb[w + (w >> 4)];
+                        win[w] = f32x2{(float)ev.re, (float)ev.im};
+                    }
+                    R pys = 0;
+                    float4* yo = (float4*)(yout + sl * N + E * t);
+#pragma unroll
+                    for (int j = 0; j < E; j += 2) {
+                        f32x2 y0 = f32x2{0.f, 0.f}, y1 = f32x2{0.f, 0.f};
+#pragma unroll
+                        for (int l = 0; l < LT; ++l) {
+                            const f32x2 e0 = win[j + LT - 1 - l], e1 = win[j + LT - l];
+                            y0 = __builtin_elementwise_fma(e0.xx, hv[l], y0);
+                            y0 = __builtin_elementwise_fma(e0.yy, hs[l], y0);
+                            y1 = __builtin_elementwise_fma(e1.xx, hv[l], y1);
+                            y1 = __builtin_elementwise_fma(e1.yy, hs[l], y1);
+                        }
+                        pys += y0.x * y0.x + y0.y * y0.y + y1.x * y1.x + y1.y * y1.y;
+                        if (yout && !(a.flags & 4)) yo[j >> 1] = float4{y0.x, y0.y, y1.x, y1.y};
+                    }
+                    if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
+                        f32x2 yp = f32x2{0.f, 0.f};
+#pragma unroll
+                        for (int l = 0; l < LT; ++l) {
+                            const C ev = row[fir_pad(R0 + t - l)];
+                            const f32x2 e = f32x2{(float)ev.re, (float)ev.im};
+                            yp = __builtin_elementwise_fma(e.xx, hv[l], yp);
+                            yp = __builtin_elementwise_fma(e.yy, hs[l], yp);
+                        }
+                        pys += yp.x * yp.x + yp.y * yp.y;
+                    }
+                    py += pys;
+                }
+                // tail for the next symbol: the last L-1 stream samples (zeros before symbol 0)
+                if (t < L - 1) tl[t] = active ? row[fir_pad(R0 + N + cp - (L - 1) + t)] : mk<R>(0, 0);
+                sym_sync<TPS>();
             } else {
                 // extended serial stream in the row: [tail (L-1) | prefix (cp) | x (N)], or with
                 // zero padding [tail (L-1) | x (N) | zeros (cp)]
@@ -523,7 +633,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                     } else {
                         b = cm.b;
                         off = k * b;
-                        ridx = nn ? (uint32_t)nn_index((double)v.re, (double)v.im, cm.lut64, cm.lut_len) : slicer(v);
+                        ridx = nn ? nn_decide<R>(v, cm) : slicer(v);
                     }
                     uint32_t d = ridx ^ tb.generic(i, b, off);
                     ses += d != 0u;

@@ -101,17 +101,38 @@ hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <typename R, int LOGN, int FB>
-static hipError_t tx_launch(const TxArgs& a, int* grid, hipStream_t s) {
-    constexpr int BLK = tx_block<FB, LOGN>();
-    const size_t sm = smem_tx<R>(LOGN, BLK, a.c.lut_len, a.c.words_per_sym, a.L, a.c.cp, FB ? tt_size(LOGN) : 0);
-    auto fn = k_tx<R, LOGN, FB>;
+template <typename R, int LOGN, int FB, int LT>
+static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
+    constexpr int BLK = tx_block<FB, LOGN, LT>();
+    TxArgs a = a0;
+    if (FB > 0 && LT > 0) {
+        // window FIR row: stream samples [-(LT-1), N+cp) at fir_pad(R0 + m)
+        const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
+        a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
+    }
+    const size_t sm = smem_tx<R>(LOGN, BLK, a.c.lut_len, a.c.words_per_sym, a.L, a.slot, FB ? tt_size(LOGN) : 0,
+                                 FB > 0 && LT > 0);
+    auto fn = k_tx<R, LOGN, FB, LT>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     const int64_t groups = (a.c.n_sym + a.chunk - 1) / a.chunk;
     *grid = clamp_grid((groups + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
+}
+
+// throughput TX by channel length: flat / window FIR (<= 4 or <= 8 taps) / run-time taps
+template <typename R, int LOGN, int FB>
+static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
+    constexpr int TPS = Geo<LOGN>::TPS;
+    if (a.L == 1) return tx_launch<R, LOGN, FB, 0>(a, grid, s);
+    if constexpr (LOGN >= 8) {
+        if (a.c.cp <= TPS) {
+            if (a.L <= 4) return tx_launch<R, LOGN, FB, 4>(a, grid, s);
+            if (a.L <= 8) return tx_launch<R, LOGN, FB, 8>(a, grid, s);
+        }
+    }
+    return tx_launch<R, LOGN, FB, -1>(a, grid, s);
 }
 
 // Throughput configuration (complex64, fixed square QAM, Philox bits; N >= 64) -> the
@@ -121,15 +142,15 @@ static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (!a.c.adaptive && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn) {
             switch (a.c.b) {
-                case 2: return tx_launch<R, LOGN, 2>(a, grid, s);
-                case 4: return tx_launch<R, LOGN, 4>(a, grid, s);
-                case 6: return tx_launch<R, LOGN, 6>(a, grid, s);
-                case 8: return tx_launch<R, LOGN, 8>(a, grid, s);
+                case 2: return tx_fast<R, LOGN, 2>(a, grid, s);
+                case 4: return tx_fast<R, LOGN, 4>(a, grid, s);
+                case 6: return tx_fast<R, LOGN, 6>(a, grid, s);
+                case 8: return tx_fast<R, LOGN, 8>(a, grid, s);
                 default: break;
             }
         }
     }
-    return tx_launch<R, LOGN, 0>(a, grid, s);
+    return tx_launch<R, LOGN, 0, -1>(a, grid, s);
 }
 
 template <typename R>

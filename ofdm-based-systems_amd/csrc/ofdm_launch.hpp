@@ -155,13 +155,14 @@ inline int tx_slot(int logn, int cp, int L) {
 // fused kernels, blk threads; tts = per-pass twiddle entries (throughput kernels) or 0
 // (the throughput kernels, tts > 0, carve no two-level twiddles and no staged bit words)
 template <typename R>
-inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int cp, int tts) {
+inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int slot, int tts, bool wfir) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn, blk);
     const int tls = L > 1 ? L - 1 : 1;
     if (tts > 0) wps = 0;
-    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(4 * sizeof(AxisInfo)) +
-           rnd16((size_t)spb * tx_slot(logn, cp, L) * c) + rnd16((size_t)spb * tls * c) +
+    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(wfir ? 32 * c : 0) +
+           rnd16(4 * sizeof(AxisInfo)) +
+           rnd16((size_t)spb * slot * c) + rnd16((size_t)spb * tls * c) +
            rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(double)) + rnd16((size_t)tts * c);
 }
 template <typename R>

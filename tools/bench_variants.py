@@ -3,7 +3,7 @@
 Times ofdm_tx / ofdm_rx with HIP events on the launch stream, throughput mode (complex64,
 bits and noise generated in the kernels), one GPU:
 
-    python tools/bench_variants.py [--symbols 200000] [--steps 5] > gpurun_out/variants.json
+    python tools/bench_variants.py [--symbols 1000000] [--steps 5] > gpurun_out/variants.json
 
 Prints one JSON object per variant and a summary table on stderr.  Which kernel runs:
 OFDM + cyclic prefix + square QAM -> the throughput specialisation; SC-OFDM, zero
@@ -43,7 +43,7 @@ VARIANTS = [
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--symbols", type=int, default=200_000)
+    ap.add_argument("--symbols", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=5)
     args = ap.parse_args()
     torch.cuda.set_device(0)
