@@ -6,7 +6,9 @@ no equaliser, AWGN at 24 dB (BER ~1e-4), complex64 arithmetic, Philox bits and
 noise generated on the device.  One step = one complete Simulation-run of the hot
 path over `--symbols` OFDM symbols per GPU (TX kernel, power all-reduce, RX
 kernel, counter all-reduce, results on the host).  Default 10 steps x 1e6
-symbols = the "1e7 symbols at one SNR" of config (b).
+symbols = the "1e7 symbols at one SNR" of config (b).  After the timed region rank 0
+also reports the BER Delta dB of the run against the reference-stream path (the second
+half of the BASELINE metric).
 
 Multi-GPU (torchrun): each rank simulates its contiguous share of the global
 symbol range of every step (weak scaling); exchanges: one all-reduce of the
@@ -86,6 +88,37 @@ def cpu_baseline(cfg, per_worker: int):
     }
 
 
+def ber_vs_reference(engine64, N, M, cp, snr, ber_phx, bits_phx, symbols=16000, seed=1):
+    """BER Delta dB of the timed throughput run against the reference-stream path at the same SNR.
+
+    The reference-stream path is the drop-in's default mode: the reference's own PCG64 bytes and
+    legacy normal draws (real array first, noise/models.py:19-21) through the complex128 kernels,
+    bit-exact with the reference NumPy code (tests/test_gpu_parity.py).  Delta dB is the
+    horizontal distance between the two BER curves at the throughput run's BER, through the
+    reference curve's local slope from a second point 0.5 dB higher; positive = the throughput
+    run needs more SNR.  Outside the timed region."""
+    b = int(np.log2(M))
+
+    def ref_ber(snr_db, sd):
+        bits = np.random.Generator(np.random.PCG64(sd)).bytes(symbols * N * b // 8)
+        rs = np.random.RandomState(sd)  # = np.random.seed(sd) + np.random.normal (the reference's draws)
+        nr = rs.normal(size=symbols * (N + cp))
+        ni = rs.normal(size=symbols * (N + cp))
+        r = engine64.run(symbols, snr_db, bits=np.frombuffer(bits, np.uint8), normals=(nr, ni))
+        return r.bit_errors, symbols * N * b
+
+    e0, n0 = ref_ber(snr, seed)
+    e1, n1 = ref_ber(snr + 0.5, seed + 1)
+    if min(e0, e1, ber_phx * bits_phx) <= 0:
+        return {"snr_db": snr, "ber": ber_phx, "ber_reference_streams": e0 / n0, "delta_db": None}
+    slope = (math.log10(e1 / n1) - math.log10(e0 / n0)) / 0.5  # decades per dB (< 0)
+    delta = (math.log10(ber_phx) - math.log10(e0 / n0)) / slope
+    sd_db = 0.4343 * math.sqrt(1.0 / e0 + 1.0 / (ber_phx * bits_phx)) / abs(slope)
+    return {"snr_db": snr, "ber": ber_phx, "ber_reference_streams": e0 / n0,
+            "reference_symbols": symbols, "slope_decades_per_db": slope,
+            "delta_db": delta, "delta_db_stderr": sd_db, "bar_db": 0.05}
+
+
 def pmc_traffic(config_name: str, symbols_per_launch: int):
     """HBM bytes per launch of the dominant kernel from a committed rocprofv3 --pmc summary
     (profiles/pmc_summary.json, produced by tools/pmc_summary.py), or None."""
@@ -110,6 +143,7 @@ def main():
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--cpu-sample", type=int, default=1500, help="OFDM symbols per CPU worker")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ber-check", action="store_true", help="skip the BER Delta-dB check vs the reference streams")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -212,6 +246,10 @@ def main():
         "path_hbm_fraction": value * 2 * kernel_bytes_per_symbol(N, b, cp) / (HBM_PEAK_GBS * 1e9 * world),
         "ber": bit_errors / (total * args.steps * N * b),
     }
+    if rank == 0 and not args.no_ber_check:
+        eng64 = LinkEngine(N, cp, h, eq, [QAMConstellationMapper(M).constellation], None, B.OFDM_F64)
+        out["ber_vs_reference"] = ber_vs_reference(eng64, N, M, cp, snr, out["ber"],
+                                                   total * args.steps * N * b)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample)
     if rank == 0:
@@ -219,6 +257,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -687,14 +687,23 @@ struct Sfc32 {
     // Two complex normals with per-component standard deviation sigma added to x0, x1, by
     // Box-Muller on the hardware transcendentals (v_log_f32 = log2, v_sin/cos_f32 take
     // revolutions): three outputs -- radius words u0, u1 (32 bits each, so the Rayleigh
-    // tail is exact to 6.7 sigma) and one angle word whose high / low 16 bits are the two
-    // phases.  x += sigma sqrt(-2 ln u) (cos 2 pi v, sin 2 pi v), u in (0, 1], v in [0, 1).
-    __device__ __forceinline__ void add_noise2(f32x2& x0, f32x2& x1, float m2s2ln2 /* -2 ln2 sigma^2 */) {
-        const float k32 = 2.3283064365386963e-10f, k16 = 1.52587890625e-05f;  // 2^-32, 2^-16
+    // tail is exact to 6.7 sigma) and one angle word a giving the two phases
+    // v0 = (a >> 9) 2^-23 (bits 9..31) and v1 = (a & 0xffff) 2^-16.
+    // x += sigma sqrt(-2 ln u) (cos 2 pi v, sin 2 pi v), u = (u32 + 1/2) 2^-32 in (0, 1).
+    // Issue-count details: -2 ln2 sigma^2 log2(u) = m2s2ln2 log2(u32 + 1/2) + c32 (one FMA,
+    // c32 = -32 m2s2ln2; |.| in the sqrt source modifier absorbs a rounding-negative
+    // argument at u -> 1), and 1 + v0 is built as a float by one v_alignbit_b32 (sin and cos
+    // have period 1 in revolutions).
+    __device__ __forceinline__ void add_noise2(f32x2& x0, f32x2& x1, float m2s2ln2 /* -2 ln2 sigma^2 */,
+                                               float c32 /* -32 m2s2ln2 */) {
+        const float k16 = 1.52587890625e-05f;  // 2^-16
         const uint32_t w0 = next(), w1 = next(), wa = next();
-        const float r0 = __builtin_amdgcn_sqrtf(m2s2ln2 * __builtin_amdgcn_logf(((float)w0 + 0.5f) * k32));
-        const float r1 = __builtin_amdgcn_sqrtf(m2s2ln2 * __builtin_amdgcn_logf(((float)w1 + 0.5f) * k32));
-        const float v0 = (float)(wa >> 16) * k16, v1 = (float)(wa & 0xFFFFu) * k16;
+        const float r0 = __builtin_amdgcn_sqrtf(
+            __builtin_fabsf(__builtin_fmaf(m2s2ln2, __builtin_amdgcn_logf((float)w0 + 0.5f), c32)));
+        const float r1 = __builtin_amdgcn_sqrtf(
+            __builtin_fabsf(__builtin_fmaf(m2s2ln2, __builtin_amdgcn_logf((float)w1 + 0.5f), c32)));
+        const float v0 = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, wa, 9));  // 1 + v0
+        const float v1 = (float)(wa & 0xFFFFu) * k16;
         x0 = __builtin_elementwise_fma(f32x2{__builtin_amdgcn_cosf(v0), __builtin_amdgcn_sinf(v0)}, f32x2{r0, r0}, x0);
         x1 = __builtin_elementwise_fma(f32x2{__builtin_amdgcn_cosf(v1), __builtin_amdgcn_sinf(v1)}, f32x2{r1, r1}, x1);
     }

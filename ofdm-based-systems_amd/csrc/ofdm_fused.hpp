@@ -512,6 +512,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
             for (int i = 0; i < E; ++i) x[i] = mk<R>(0, 0);
         }
         const float m2s2ln2 = -1.3862943611198906f * (float)sigma * (float)sigma;
+        const float c32 = -32.0f * m2s2ln2;
         if (active && array_noise) {
             const double* nr = a.nr + sg * (N + cp) + (zp ? 0 : cp);
             const double* ni = a.ni + sg * (N + cp) + (zp ? 0 : cp);
@@ -525,17 +526,17 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
 #pragma unroll
             for (int i = 0; i + 1 < E; i += 2) {
                 if constexpr (sizeof(R) == 4) {
-                    tb.g.add_noise2(x[i].v, x[i + 1].v, m2s2ln2);
+                    tb.g.add_noise2(x[i].v, x[i + 1].v, m2s2ln2, c32);
                 } else {
                     f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
-                    tb.g.add_noise2(n0, n1, m2s2ln2);
+                    tb.g.add_noise2(n0, n1, m2s2ln2, c32);
                     x[i] = x[i] + mk<R>((R)n0.x, (R)n0.y);
                     x[i + 1] = x[i + 1] + mk<R>((R)n1.x, (R)n1.y);
                 }
             }
             if constexpr (E == 1) {
                 f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
-                tb.g.add_noise2(n0, n1, m2s2ln2);
+                tb.g.add_noise2(n0, n1, m2s2ln2, c32);
                 x[0] = x[0] + mk<R>((R)n0.x, (R)n0.y);
             }
         }
@@ -552,7 +553,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                         v.im += sigma * (R)a.ni[sg * (N + cp) + N + k];
                     } else if (noise) {
                         f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
-                        tb.g.add_noise2(n0, n1, m2s2ln2);
+                        tb.g.add_noise2(n0, n1, m2s2ln2, c32);
                         v = v + mk<R>((R)n0.x, (R)n0.y);
                     }
                     x[i] = x[i] + v;

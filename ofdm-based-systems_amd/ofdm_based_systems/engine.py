@@ -87,7 +87,10 @@ class LinkEngine:
         return B.stream_ptr()
 
     def upload(self, a: np.ndarray) -> torch.Tensor:
-        return torch.from_numpy(np.ascontiguousarray(a)).to(self.device())
+        a = np.ascontiguousarray(a)
+        if not a.flags.writeable:  # e.g. np.frombuffer(bytes): torch wants a writable array
+            a = a.copy()
+        return torch.from_numpy(a).to(self.device())
 
     def valid_bits(self, n_sym: int) -> int:
         """Bits the reference compares: all of them in FIXED mode, whole bytes in adaptive mode

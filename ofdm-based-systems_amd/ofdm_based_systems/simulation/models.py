@@ -5,10 +5,10 @@ keys.  ``run()`` keeps the reference's setup (channel, prefix length, power
 allocation, bit loading -- host precompute on <= 4096 values) and replaces the
 data path with the fused GPU engine (:mod:`ofdm_based_systems.engine`):
 
-* OFDM + cyclic/no prefix + square QAM (FIXED or CAPACITY_BASED): two fused
-  kernels (ofdm_tx / ofdm_rx);
-* SC-OFDM, zero padding or PSK: the GPU operators composed as in the reference
-  (encode -> modulate -> transmit -> demodulate -> decode), compared on the GPU.
+* every built-in modulator / prefix / constellation (OFDM or SC-OFDM, cyclic, zero or no
+  prefix, QAM or PSK, FIXED or CAPACITY_BASED): the two fused kernels (ofdm_tx / ofdm_rx);
+* a user-supplied strategy class: the GPU operators composed as in the reference
+  (encode -> modulate -> transmit -> demodulate -> decode), calling its own methods.
 
 ``rng_mode='reference'`` (default) draws the bits (PCG64 ``Generator.bytes``) and
 the AWGN normals (legacy ``np.random.normal``, real part first) exactly as the

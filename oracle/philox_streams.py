@@ -23,9 +23,9 @@ TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS for i < E)
   bits 8*(i & 3).. of output i >> 2);
 * noise: outputs 4+3j, 5+3j, 6+3j give elements 2j, 2j+1: radius words u0, u1, angle word
   a; element 2j+q gets sigma*sqrt(-2 ln((u_q + 0.5) 2^-32)) * exp(2 pi i v_q) with
-  v_0 = (a >> 16) 2^-16, v_1 = (a & 0xffff) 2^-16, added to the kept time sample k.
-  (float32 arithmetic on the GPU; here the radius argument follows the same float32
-  rounding and the rest is evaluated in float64.)
+  v_0 = (a >> 9) 2^-23 (bits 9..31), v_1 = (a & 0xffff) 2^-16, added to the kept time
+  sample k.  (float32 arithmetic on the GPU; here the radius argument follows the same
+  float32 rounding of u32 + 0.5 and the rest is evaluated in float64.)
 """
 
 from __future__ import annotations
@@ -117,7 +117,7 @@ def lane_noise(gen: Sfc32, S: int, N: int, sigma: float) -> np.ndarray:
     for _ in range((E + 1) // 2):
         u = [gen.next(), gen.next()]
         a = gen.next()
-        v = [(a >> np.uint32(16)).astype(np.float64) * 2.0 ** -16, (a & np.uint32(0xFFFF)).astype(np.float64) * 2.0 ** -16]
+        v = [(a >> np.uint32(9)).astype(np.float64) * 2.0 ** -23, (a & np.uint32(0xFFFF)).astype(np.float64) * 2.0 ** -16]
         for q in range(2):
             uf = (u[q].astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -32)
             r = np.sqrt(np.float64(m2s2ln2) * np.log2(uf.astype(np.float64)))
@@ -200,4 +200,4 @@ def lane_noise_tail(gen: Sfc32, sigma: float) -> np.ndarray:
     a = gen.next()
     uf = (u[0].astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -32)
     r = np.sqrt(np.float64(m2s2ln2) * np.log2(uf.astype(np.float64)))
-    return r * np.exp(2j * np.pi * (a >> np.uint32(16)).astype(np.float64) * 2.0 ** -16)
+    return r * np.exp(2j * np.pi * (a >> np.uint32(9)).astype(np.float64) * 2.0 ** -23)
