@@ -12,12 +12,13 @@
  * Conventions
  *  - Every buffer argument is a DEVICE pointer owned by the caller (PyTorch
  *    allocates it).  The library owns only plan-scoped constant tables and a
- *    small partial-sum workspace.
+ *    small partial-sum workspace per stream the plan is used on.
  *  - Complex arrays are interleaved (re, im) in the plan's precision:
  *    OFDM_F32 -> float2 (complex64), OFDM_F64 -> double2 (complex128).
  *  - Every call is asynchronous on the given hipStream_t (NULL = default stream);
- *    no call synchronises the device.  A plan must not be used from two host
- *    threads at once (its workspace is shared).
+ *    no call synchronises the device.  One plan may be used on several streams
+ *    whose work overlaps (the reductions keep one workspace per stream); it must
+ *    not be used on the SAME stream from two host threads at once.
  *  - Return 0 on success, a negative OFDM_E* code on failure; the message is in
  *    ofdm_last_error() (thread-local).  Nothing throws across the ABI.
  *  - Bits are packed MSB-first in bytes (simulation/models.py:59-69,

@@ -10,7 +10,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -94,7 +96,13 @@ struct ofdm_plan_s {
     int n, logn, cp, prec, eq, L;
     int adaptive, b, bps, n_axis, lut_len, n_active;
     double gain_mean;
-    DevBuf tw, ptw, lut, lut64, h, eq_a, eq_b, axis, sc, active, ws, H64;
+    DevBuf tw, ptw, lut, lut64, h, eq_a, eq_b, axis, sc, active, H64;
+    // partial-sum workspaces (3 x kMaxGrid doubles), one per HIP stream the plan has been
+    // used on: launches on different streams may run concurrently, and a reduction's
+    // partials must not be overwritten by another stream's kernel before k_finalize reads
+    // them.  Same-stream launches are ordered, so one record per stream is enough.
+    std::mutex ws_mu;
+    std::map<void*, DevBuf> ws;
     int has_const, has_channel, separable, zp, single_carrier;
     size_t csize() const { return prec == OFDM_F32 ? 8 : 16; }
 };
@@ -355,7 +363,6 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
         HIPCHK(hipStreamSynchronize(s));
         p->gain_mean = gs / p->n;
     }
-    if (hipMalloc(&p->ws.p, sizeof(double) * 3 * kMaxGrid) != hipSuccess) return fail(OFDM_E_ALLOC, "hipMalloc failed");
     HIPCHK(hipStreamSynchronize(s));
     *out = guard.release();
     return OFDM_OK;
@@ -533,8 +540,20 @@ int ofdm_nn_classify(void* stream, const double* lut, int32_t m, const void* z, 
     return OFDM_OK;
 }
 
-static int reduce_into(ofdm_plan_t p, hipStream_t s, int grid, int nfields, int max_mask, double* stats) {
-    HIPCHK(launch_finalize((const double*)p->ws.p, grid, nfields, max_mask, stats, s));
+// The stream's partial-sum workspace (allocated on first use), or nullptr.
+static double* workspace(ofdm_plan_t p, void* stream) {
+    std::lock_guard<std::mutex> lk(p->ws_mu);
+    DevBuf& d = p->ws[stream];
+    if (!d.p && hipMalloc(&d.p, sizeof(double) * 3 * kMaxGrid) != hipSuccess) {
+        d.p = nullptr;
+        return nullptr;
+    }
+    return (double*)d.p;
+}
+
+static int reduce_into(ofdm_plan_t p, hipStream_t s, const double* ws, int grid, int nfields, int max_mask,
+                       double* stats) {
+    HIPCHK(launch_finalize(ws, grid, nfields, max_mask, stats, s));
     return OFDM_OK;
 }
 
@@ -543,11 +562,13 @@ int ofdm_channel(ofdm_plan_t p, void* stream, const void* sig, int64_t len, void
     if (len < 0 || (len > 0 && (!sig || !y))) return fail(OFDM_E_INVALID, "bad argument to ofdm_channel");
     if (len == 0) return OFDM_OK;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((len + 255) / 256, kMaxGrid));
-    ConvArgs a{sig, y, len, p->h.p, p->L, (double*)p->ws.p};
+    double* ws = workspace(p, stream);
+    if (!ws) return fail(OFDM_E_ALLOC, "hipMalloc failed");
+    ConvArgs a{sig, y, len, p->h.p, p->L, ws};
 #define CALL(R) launch_conv<R>(a, grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));
 #undef CALL
-    if (power_sum) return reduce_into(p, (hipStream_t)stream, grid, 1, 0, power_sum);
+    if (power_sum) return reduce_into(p, (hipStream_t)stream, ws, grid, 1, 0, power_sum);
     return OFDM_OK;
 }
 
@@ -555,11 +576,13 @@ int ofdm_power(ofdm_plan_t p, void* stream, const void* y, int64_t len, double* 
     if (!p || len < 0 || (len > 0 && !y) || !power_sum) return fail(OFDM_E_INVALID, "bad argument to ofdm_power");
     if (len == 0) return OFDM_OK;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((len + 255) / 256, kMaxGrid));
-    PowerArgs a{y, len, (double*)p->ws.p};
+    double* ws = workspace(p, stream);
+    if (!ws) return fail(OFDM_E_ALLOC, "hipMalloc failed");
+    PowerArgs a{y, len, ws};
 #define CALL(R) launch_power<R>(a, grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));
 #undef CALL
-    return reduce_into(p, (hipStream_t)stream, grid, 1, 0, power_sum);
+    return reduce_into(p, (hipStream_t)stream, ws, grid, 1, 0, power_sum);
 }
 
 int ofdm_awgn(ofdm_plan_t p, void* stream, void* y, int64_t len, const double* nr, const double* ni,
@@ -615,7 +638,8 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
     // the bits buffer covers global symbols [0, sym0 + n_sym)
     fill_common(p, a.c, bits, seed, sym0, n_sym, sym0 + n_sym);
     a.y = y;
-    a.partials = (double*)p->ws.p;
+    a.partials = workspace(p, stream);
+    if (!a.partials) return fail(OFDM_E_ALLOC, "hipMalloc failed");
     a.h = p->h.p;
     a.L = p->L;
     a.chunk = p->L > 1 ? 16 : 1;
@@ -625,7 +649,7 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
 #define CALL(R) launch_tx<R>(p->logn, a, &grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));
 #undef CALL
-    return reduce_into(p, (hipStream_t)stream, grid, 3, 4, stats);
+    return reduce_into(p, (hipStream_t)stream, a.partials, grid, 3, 4, stats);
 }
 
 int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const double* ni, uint64_t seed,

@@ -205,17 +205,24 @@ class LinkEngine:
             import torch.distributed as dist
 
             dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
-        return PendingLink(n_sym, samples, stats, counters, z_out)
+        done = None
+        if dev.type == "cuda":
+            done = torch.cuda.Event()
+            done.record()  # on the launch stream: result() may be called under another stream
+        return PendingLink(n_sym, samples, stats, counters, z_out, done)
 
 
 class PendingLink:
     """Device-side results of one :meth:`LinkEngine.run_async` call."""
 
-    def __init__(self, n_sym, samples, stats, counters, z_out):
+    def __init__(self, n_sym, samples, stats, counters, z_out, done=None):
         self.n_sym, self.samples = n_sym, samples
         self.stats, self.counters, self.z_out = stats, counters, z_out
+        self.done = done
 
     def result(self) -> LinkStats:
+        if self.done is not None:
+            self.done.synchronize()
         st = self.stats.cpu().numpy()
         cnt = self.counters.cpu().numpy()
         samples = self.samples

@@ -24,7 +24,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from ofdm_based_systems import _backend as B  # noqa: E402
+from ofdm_based_systems.constellation.adaptive import AdaptiveConstellationMapper  # noqa: E402
 from ofdm_based_systems.constellation.models import PSKConstellationMapper, QAMConstellationMapper  # noqa: E402
+from ofdm_based_systems.power_allocation.models import WaterfillingPowerAllocation  # noqa: E402
 from ofdm_based_systems.engine import LinkEngine  # noqa: E402
 
 EQ = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}
@@ -33,6 +35,7 @@ EQ = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}
 VARIANTS = [
     ("b: OFDM CP 64-QAM flat", 1024, 64, "QAM", "flat_fading", "NONE", 24.0, "OFDM", "CP"),
     ("c: OFDM CP 64-QAM severe MMSE", 1024, 64, "QAM", "severe_multipath", "MMSE", 27.75, "OFDM", "CP"),
+    ("d: adaptive QAM N=2048 P1 MMSE WF", 2048, 0, "ADAPTIVE", "Lin-Phoong_P1", "MMSE", 20.0, "OFDM", "CP"),
     ("e: OFDM CP 256-QAM N=4096 P1 MMSE", 4096, 256, "QAM", "Lin-Phoong_P1", "MMSE", 30.0, "OFDM", "CP"),
     ("f1: SC-OFDM CP 64-QAM severe MMSE", 1024, 64, "QAM", "severe_multipath", "MMSE", 27.75, "SC", "CP"),
     ("f2: OFDM ZP 64-QAM severe MMSE", 1024, 64, "QAM", "severe_multipath", "MMSE", 27.75, "OFDM", "ZP"),
@@ -41,18 +44,41 @@ VARIANTS = [
 ]
 
 
+def adaptive_tables(N, h, snr_db, ser=1e-3):
+    """Config (d): CAPACITY_BASED bit loading over the water-filling allocation with P_tot = N
+    (simulation/models.py:289-395, as Simulation.run computes it): per-subcarrier QAM orders
+    from calculate_bit_loading_order, their LUTs and the subcarrier -> LUT table."""
+    gains = np.abs(np.fft.fft(h, N)) ** 2
+    noise_power = 10 ** (-snr_db / 10)
+    alloc = WaterfillingPowerAllocation(N, gains, noise_power).allocate()
+    orders = np.array([QAMConstellationMapper.calculate_bit_loading_order(ser=ser, snr=p * g / noise_power)
+                       for p, g in zip(alloc, gains)], dtype=np.int64)
+    mapper = AdaptiveConstellationMapper(orders, QAMConstellationMapper, N)
+    luts, sc = mapper.lut_tables()
+    return luts, sc, int(np.sum(mapper.get_bits_per_subcarrier()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--symbols", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--only", default="", help="comma-separated variant name prefixes (e.g. b,d)")
     args = ap.parse_args()
+    only = [o for o in args.only.split(",") if o]
     torch.cuda.set_device(0)
     rows = []
     for name, N, M, scheme, ch, eq, snr, mod, pre in VARIANTS:
+        if only and not any(name.split(":")[0] == o for o in only):
+            continue
         h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
         cp = len(h) - 1
-        lut = (QAMConstellationMapper(M) if scheme == "QAM" else PSKConstellationMapper(M)).constellation
-        eng = LinkEngine(N, cp, h, EQ[eq], [lut], None, B.OFDM_F32,
+        sc = None
+        if scheme == "ADAPTIVE":
+            luts, sc, bps = adaptive_tables(N, h, snr)
+            M = 2.0 ** (bps / N)  # mean bits per subcarrier, for the BER denominator
+        else:
+            luts = [(QAMConstellationMapper(M) if scheme == "QAM" else PSKConstellationMapper(M)).constellation]
+        eng = LinkEngine(N, cp, h, EQ[eq], luts, sc, B.OFDM_F32,
                          prefix=B.PREFIX_ZERO if pre == "ZP" else B.PREFIX_CYCLIC,
                          modulator=B.MOD_SC if mod == "SC" else B.MOD_OFDM)
         S = args.symbols if N <= 1024 else args.symbols // (N // 1024)
