@@ -20,7 +20,8 @@ TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS for i < E)
   Philox4x32-10 block, key = (seed mod 2^32, seed >> 32), counter = (t, s mod 2^32,
   s >> 32, 0x1A7E5EED);
 * payload: outputs 0..3 are 128 bits; element i takes the low b bits of byte i (byte i =
-  bits 8*(i & 3).. of output i >> 2);
+  bits 8*(i & 3).. of output i >> 2); with adaptive bit loading b = b_k of its subcarrier
+  (b_k = 0: the subcarrier is unused and carries 0+0j);
 * noise: outputs 4+3j, 5+3j, 6+3j give elements 2j, 2j+1: radius words u0, u1, angle word
   a; element 2j+q gets sigma*sqrt(-2 ln((u_q + 0.5) 2^-32)) * exp(2 pi i v_q) with
   v_0 = (a >> 9) 2^-23 (bits 9..31), v_1 = (a & 0xffff) 2^-16, added to the kept time
@@ -99,13 +100,15 @@ def _lane_to_row(v: np.ndarray, S: int, N: int) -> np.ndarray:
     return v.reshape(S, tps, E).transpose(0, 2, 1).reshape(S, N)
 
 
-def tx_indices(gen: Sfc32, S: int, N: int, b: int) -> np.ndarray:
-    """Constellation indices (S, N) from outputs 0..3 of every lane generator."""
+def tx_indices(gen: Sfc32, S: int, N: int, b) -> np.ndarray:
+    """Constellation indices (S, N) from outputs 0..3 of every lane generator; b is the bits
+    per subcarrier, one value or one per subcarrier (adaptive loading)."""
     E, _ = geometry(N)
     words = np.stack([gen.next() for _ in range(4)], axis=1)  # (lanes, 4)
     i = np.arange(E)
-    idx = (words[:, i >> 2] >> (8 * (i & 3)).astype(np.uint32)) & np.uint32((1 << b) - 1)
-    return _lane_to_row(idx.astype(np.int64), S, N)
+    byte = (words[:, i >> 2] >> (8 * (i & 3)).astype(np.uint32)) & np.uint32(0xFF)
+    mask = (np.int64(1) << np.broadcast_to(np.asarray(b, np.int64), (N,))) - 1
+    return _lane_to_row(byte.astype(np.int64), S, N) & mask[None, :]
 
 
 def lane_noise(gen: Sfc32, S: int, N: int, sigma: float) -> np.ndarray:
@@ -139,20 +142,35 @@ class PhiloxLink:
 
 def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq: str, snr_db: float,
                noise_on: bool = True, modulator: str = "OFDM", prefix: str = "CP",
-               scheme: str = "QAM") -> PhiloxLink:
+               scheme: str = "QAM", orders=None) -> PhiloxLink:
     """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic.
 
     modulator "OFDM" | "SC" (modulation/models.py:58-91), prefix "CP" | "ZP"
     (prefix/models.py:29-101), scheme "QAM" | "PSK".  With zero padding every lane draws,
     after its elements' noise, one more noise triple per received tail sample
     N + k (k = t + i*TPS < cp, in order of i) and uses its first sample.
+
+    orders: per-subcarrier QAM orders (CAPACITY_BASED bit loading, 0 = unused; M is then
+    ignored).  As in the reference's decode (constellation/adaptive.py:259-263) a trailing
+    partial byte of the whole run's bit stream is not compared; symbol errors count every
+    used subcarrier.
     """
-    b = int(np.log2(M))
-    lut = O.qam_lut(M) if scheme == "QAM" else O.psk_lut(M)
     E, tps = geometry(N)
     gen = lane_generators(seed, np.arange(S), N)
-    idx = tx_indices(gen, S, N, b)
-    X = lut[idx]
+    if orders is not None:
+        orders = np.asarray(orders, np.int64)
+        bk = np.array([int(np.log2(o)) if o > 0 else 0 for o in orders], np.int64)
+        idx = tx_indices(gen, S, N, bk)
+        luts = {int(o): O.qam_lut(int(o)) for o in np.unique(orders) if o > 0}
+        X = np.zeros((S, N), np.complex128)
+        for o, lt in luts.items():
+            cols = orders == o
+            X[:, cols] = lt[idx[:, cols]]
+    else:
+        b = int(np.log2(M))
+        lut = O.qam_lut(M) if scheme == "QAM" else O.psk_lut(M)
+        idx = tx_indices(gen, S, N, b)
+        X = lut[idx]
     s_t = np.fft.ifft(X, axis=1, norm="ortho") if modulator == "OFDM" else X
     if prefix == "ZP":
         x = np.concatenate([s_t, np.zeros((S, cp), np.complex128)], axis=1)
@@ -185,6 +203,24 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     Z = O.equalize(np.fft.fft(rxs, axis=1, norm="ortho"), H, eq, snr_db)
     if modulator == "SC":
         Z = np.fft.ifft(Z, axis=1, norm="ortho")
+    if orders is not None:
+        ridx = np.zeros((S, N), np.int64)
+        for o, lt in luts.items():
+            cols = np.flatnonzero(orders == o)
+            ridx[:, cols] = O.nn_demap(Z[:, cols].ravel(), lt).reshape(S, len(cols))
+        diff = (ridx ^ idx).astype(np.int64)
+        # stream position of bit j (MSB first) of subcarrier k in symbol s: s*tot + off_k + j
+        tot = int(bk.sum())
+        valid = (S * tot // 8) * 8
+        off = np.concatenate([[0], np.cumsum(bk)[:-1]])
+        be = 0
+        for j in range(int(bk.max(initial=0))):
+            has = bk > j
+            bit = (diff >> np.maximum(bk - 1 - j, 0)[None, :]) & 1
+            pos = np.arange(S)[:, None] * tot + (off + j)[None, :]
+            be += int(np.count_nonzero(bit.astype(bool) & has[None, :] & (pos < valid)))
+        se = int(np.count_nonzero(diff[:, bk > 0]))
+        return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk)
     ridx = O.nn_demap(Z.ravel(), lut).reshape(S, N)
     diff = (ridx ^ idx).astype(np.uint64)
     be = int(sum(int(np.count_nonzero((diff >> np.uint64(j)) & np.uint64(1))) for j in range(b)))

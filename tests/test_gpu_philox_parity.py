@@ -25,6 +25,8 @@ from conftest import channel
 import philox_streams as P
 import ofdm_oracle as O
 from ofdm_based_systems import _backend as B
+from ofdm_based_systems.constellation.adaptive import AdaptiveConstellationMapper
+from ofdm_based_systems.constellation.models import QAMConstellationMapper
 from ofdm_based_systems.engine import LinkEngine
 
 pytestmark = pytest.mark.gpu
@@ -47,6 +49,14 @@ CASES = [
     (256, 8, "Lin-Phoong_P1", "MMSE", 512, 17.0, B.OFDM_F32, {"scheme": "PSK"}),
     (128, 4, "Lin-Phoong_P2", "MMSE", 1024, 10.0, B.OFDM_F64, {"modulator": "SC", "prefix": "ZP", "scheme": "PSK"}),
     (2048, 16, "Lin-Phoong_P1", "MMSE", 128, 19.0, B.OFDM_F32, {"prefix": "ZP", "modulator": "SC"}),
+    # CAPACITY_BASED bit loading (config d): per-subcarrier orders from water-filling at the SNR;
+    # an odd symbol count leaves a trailing partial byte that is not compared
+    (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F32, {"adaptive": True}),
+    (1024, 0, "severe_multipath", "ZF", 257, 22.0, B.OFDM_F32, {"adaptive": True}),
+    (256, 0, "two_ray", "ZF", 1023, 30.0, B.OFDM_F32, {"adaptive": True}),   # up to 256-QAM
+    (256, 0, "two_ray", "MMSE", 1024, 16.0, B.OFDM_F32, {"adaptive": True}),  # unused subcarriers
+    (4096, 0, "Lin-Phoong_P1", "MMSE", 160, 26.0, B.OFDM_F32, {"adaptive": True}),
+    (64, 0, "default_multipath", "MMSE", 2049, 18.0, B.OFDM_F32, {"adaptive": True}),
 ]
 
 
@@ -58,20 +68,27 @@ def _id(c):
 IDS = [_id(c) for c in CASES]
 
 
-def setup(N, M, ch, eq, prec, var=None):
-    var = var or {}
+def setup(N, M, ch, eq, prec, var=None, snr=None):
+    """Engine of a case; returns (engine, CIR, cp, keyword arguments for P.run_philox)."""
+    var = dict(var or {})
     h = channel(ch)
     cp = len(h) - 1
-    lut = O.psk_lut(M) if var.get("scheme") == "PSK" else O.qam_lut(M)
-    eng = LinkEngine(N, cp, h, EQ[eq], [lut], None, prec,
+    sc = None
+    if var.pop("adaptive", False):
+        orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
+        luts, sc = AdaptiveConstellationMapper(orders, QAMConstellationMapper, N).lut_tables()
+        var["orders"] = orders
+    else:
+        luts = [O.psk_lut(M) if var.get("scheme") == "PSK" else O.qam_lut(M)]
+    eng = LinkEngine(N, cp, h, EQ[eq], luts, sc, prec,
                      prefix=B.PREFIX_ZERO if var.get("prefix") == "ZP" else B.PREFIX_CYCLIC,
                      modulator=B.MOD_SC if var.get("modulator") == "SC" else B.MOD_OFDM)
-    return eng, h, cp
+    return eng, h, cp, var
 
 
 @pytest.mark.parametrize("N,M,ch,eq,S,snr,prec,var", CASES, ids=IDS)
 def test_tx_samples_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
-    eng, h, cp = setup(N, M, ch, eq, prec, var)
+    eng, h, cp, var = setup(N, M, ch, eq, prec, var, snr)
     seed = 1234
     y = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
     stats = torch.zeros(3, dtype=torch.float64, device="cuda")
@@ -92,7 +109,7 @@ def test_tx_samples_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
 
 @pytest.mark.parametrize("N,M,ch,eq,S,snr,prec,var", CASES, ids=IDS)
 def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
-    eng, h, cp = setup(N, M, ch, eq, prec, var)
+    eng, h, cp, var = setup(N, M, ch, eq, prec, var, snr)
     seed = 77
     res = eng.run(S, snr, seed=seed)
     ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, **var)
@@ -104,7 +121,7 @@ def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
 
 def test_sharded_halves_add_up_to_the_whole(gpu):
     """Symbols [0, S) in two launches at different offsets = one launch (stream is per symbol)."""
-    eng, h, cp = setup(1024, 64, "severe_multipath", "MMSE", B.OFDM_F32)
+    eng, h, cp, _ = setup(1024, 64, "severe_multipath", "MMSE", B.OFDM_F32)
     S = 600
     whole = eng.run(S, 24.0, seed=9)
     y = torch.empty((S, 1024), dtype=eng.cdtype, device="cuda")
