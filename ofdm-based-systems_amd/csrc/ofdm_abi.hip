@@ -104,6 +104,7 @@ struct ofdm_plan_s {
     std::mutex ws_mu;
     std::map<void*, DevBuf> ws;
     int has_const, has_channel, separable, zp, single_carrier;
+    int upat;  // all LUTs use the reference's square-QAM level -> index patterns (kUPat)
     size_t csize() const { return prec == OFDM_F32 ? 8 : 16; }
 };
 
@@ -168,6 +169,22 @@ int build_axis(const double* lut, int m, int lut_off, AxisInfo& ax) {
         ax.qpat[k] = (uint8_t)qset[k];
     }
     return OFDM_OK;
+}
+
+// True when every axis maps levels to index bits like the reference's square-QAM LUTs:
+// ipat[k] = U[k], qpat[k] = U[side - 1 - k] (ofdm_device.hpp, kUPat), at most 4 LUTs.
+bool universal_patterns(const std::vector<AxisInfo>& axes) {
+    if (axes.empty() || axes.size() > 4) return false;
+    for (const AxisInfo& ax : axes) {
+        if (ax.side < 2 || ax.side > 16) return false;
+        for (int k = 0; k < ax.side; ++k) {
+            const uint32_t u = (kUPat[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            const int kq = ax.side - 1 - k;
+            const uint32_t uq = (kUPat[kq >> 2] >> (8 * (kq & 3))) & 0xFFu;
+            if (ax.ipat[k] != u || ax.qpat[k] != uq) return false;
+        }
+    }
+    return true;
 }
 
 // Diagnostic ablation switches for timing studies (tools/ablate.py); unset = 0 = normal run.
@@ -282,6 +299,7 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
         p->n_axis = d->n_luts;
         p->separable = 1;
         for (const AxisInfo& ax : axes) p->separable &= ax.side > 0;
+        p->upat = p->separable && universal_patterns(axes);
         std::vector<double> pool(d->lut_pool, d->lut_pool + 2 * off);
         if ((rc = upload_cpx(p->lut, pool, p->prec, s))) return rc;
         if ((rc = upload(p->lut64, pool.data(), pool.size(), s))) return rc;
@@ -625,6 +643,7 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
     c.nn = !p->separable;
     c.ystride = c.zpad ? p->n + p->cp : p->n;
     c.lut64 = (const double*)p->lut64.p;
+    c.upat = p->upat;
 }
 
 int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int64_t sym0, int64_t n_sym,

@@ -557,6 +557,71 @@ struct PermSlicer {
     }
 };
 
+// ------------------------------------------------------------------ adaptive throughput slicer
+// The reference's square-QAM LUTs (constellation/models.py:180-218) share one level -> index
+// pattern for every order: ipat_M[k] is the first sqrt(M) entries of
+// U = [0 1 3 2 7 6 4 5 15 14 12 13 8 9 11 10], and qpat_M[k] = U[sqrt(M) - 1 - k] (the Q
+// levels run the other way; the plan checks both, ofdm_abi.hip:universal_patterns).  So a
+// per-subcarrier order changes only the level scale, the clamp and the bit split: the Q level
+// is taken on -Im z, both axes look up U, and the Q bits move up by b_k/2.
+constexpr uint32_t kUPat[4] = {0x02030100u, 0x05040607u, 0x0D0C0E0Fu, 0x0A0B0908u};
+
+// byte j of the result = U[byte j of sel] (bytes of sel < 16)
+__device__ __forceinline__ uint32_t upat_lookup(uint32_t sel) {
+    const uint32_t s7 = sel & 0x07070707u;
+    const uint32_t lo = __builtin_amdgcn_perm(kUPat[1], kUPat[0], s7);
+    const uint32_t hi = __builtin_amdgcn_perm(kUPat[3], kUPat[2], s7);
+    const uint32_t m = __builtin_amdgcn_perm(sel << 12, sel << 4, 0x090B080Au);  // 0xff where bit 3 set
+    return (hi & m) | (lo & ~m);
+}
+
+// Per-order slicer constants in LDS (one entry per LUT of the plan, entry 7 = unused
+// subcarrier): level coordinate y = z * mul + add, clamp bound MAGIC + side - 1, and
+// meta = tx bit mask (1 << b) - 1 | (1 << b/2) << 8.
+struct OrderParams {
+    float mul, add;
+    uint32_t smax, meta;
+};
+constexpr int kUnusedOrder = 7;
+
+// (rx ^ tx) of four elements of possibly different orders, one per byte.  op[j] = the
+// element's order entry, txw = the lane word; mask_out = the tx masks (byte j).
+__device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], const OrderParams* const (&op)[4],
+                                                  uint32_t txw) {
+    constexpr int MAGIC = 0x4B400000;  // bit pattern of 1.5 * 2^23: round(y) in the low mantissa
+    uint32_t li[4], lq[4], meta[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float mul = op[j]->mul, add = op[j]->add;
+        // level coordinates Re z * mul + add and -Im z * mul + add
+        const float fx = __builtin_fmaf(z[j].re, mul, add) + 12582912.0f;
+        const float fy = __builtin_fmaf(-z[j].im, mul, add) + 12582912.0f;
+        const int smax = (int)op[j]->smax;
+        li[j] = (uint32_t)min(max(__builtin_bit_cast(int, fx), MAGIC), smax);
+        lq[j] = (uint32_t)min(max(__builtin_bit_cast(int, fy), MAGIC), smax);
+        // opaque to the v_perm byte-provider combine, which otherwise merges the Q gather
+        // into the I gather (seen with run-time clamp bounds: the Q axis vanished)
+        asm("" : "+v"(li[j]), "+v"(lq[j]));
+        meta[j] = op[j]->meta;
+    }
+    const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
+                                              __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
+    const uint32_t sq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(lq[3], lq[2], 0x0c0c0400u),
+                                              __builtin_amdgcn_perm(lq[1], lq[0], 0x0c0c0400u), 0x05040100u);
+    const uint32_t ib = upat_lookup(si), qb = upat_lookup(sq);
+    // Q bits << b_j/2 per byte: bytes 0, 2 and 1, 3 as u16 pairs through v_pk_mul_lo_u16
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t w02 = __builtin_amdgcn_perm(0u, qb, 0x0c020c00u), w13 = __builtin_amdgcn_perm(0u, qb, 0x0c030c01u);
+    const uint32_t f02 = __builtin_amdgcn_perm(meta[2], meta[0], 0x0c050c01u);
+    const uint32_t f13 = __builtin_amdgcn_perm(meta[3], meta[1], 0x0c050c01u);
+    const uint32_t p02 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, w02) * __builtin_bit_cast(u16x2, f02));
+    const uint32_t p13 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, w13) * __builtin_bit_cast(u16x2, f13));
+    const uint32_t qs = __builtin_amdgcn_perm(p13, p02, 0x06020400u);
+    const uint32_t mw = __builtin_amdgcn_perm(__builtin_amdgcn_perm(meta[3], meta[2], 0x0c0c0400u),
+                                              __builtin_amdgcn_perm(meta[1], meta[0], 0x0c0c0400u), 0x05040100u);
+    return (ib | qs) ^ (txw & mw);
+}
+
 // ------------------------------------------------------------------ reductions
 // Sum over the TPS threads of one symbol group (t = threadIdx.x % TPS).  All threads
 // of the workgroup must call it (uses a workgroup barrier for TPS > 64).

@@ -11,8 +11,9 @@
 //
 // Specialisations: FB = 2/4/6/8 selects the throughput kernel (fixed square QAM with
 // b = FB bits, Philox-keyed bits and noise, complex64) with everything else compiled
-// out; FB = 0 is the generic kernel (reference-mode bytes and normals, adaptive bit
-// loading, complex128).
+// out; FB = 1 is the throughput kernel for adaptive bit loading (per-subcarrier square-QAM
+// orders, CAPACITY_BASED); FB = 0 is the generic kernel (reference-mode bytes and normals,
+// SC-OFDM, zero padding, PSK, complex128).
 #pragma once
 
 #include <type_traits>
@@ -22,6 +23,13 @@
 // TX_WAVES / RX_WAVES) for occupancy studies.
 #ifndef OFDM_TX_WAVES
 #define OFDM_TX_WAVES 3
+#endif
+// throughput TX with the register-window FIR (LT = 4 / 8): 2 waves/SIMD (256 registers) --
+// at 3 the window, the taps and the FFT state spill (54 VGPRs at LT = 8); measured on MI355X:
+// config (c) TX 3.71 -> 2.94 ms, (e) 14.1 -> 12.5 ms per 1e6 symbols, while the generic kernel
+// is faster at 3 (SC-OFDM TX 3.57 vs 4.33 ms)
+#ifndef OFDM_TX_WFIR_WAVES
+#define OFDM_TX_WFIR_WAVES 2
 #endif
 #ifndef OFDM_RX_WAVES
 #define OFDM_RX_WAVES 1
@@ -51,7 +59,7 @@ constexpr int tx_block() {
 // padded FIR row index of the throughput multipath TX: one slot per 16 elements
 __host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
 template <int FB, int LOGN, int EQ>
-constexpr int rx_block() { return FB > 0 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock; }
+constexpr int rx_block() { return FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock; }
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 
 // Reference mode: stage OFDM symbol s's tx bits from the packed bytes of the run
@@ -191,7 +199,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()), (block_waves(tx_block<F
     const int tls = L > 1 ? L - 1 : 1;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
-    C* lut = cv.take<C>(cm.lut_len);
+    C* lut = cv.take<C>(cm.lut_len + (FB == 1));
     C* h = cv.take<C>(32);
     C* hsw = cv.take<C>(WFIR ? 32 : 0);  // window FIR: the taps swizzled, (-im, re)
     AxisInfo* axis = cv.take<AxisInfo>(4);
@@ -201,12 +209,23 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()), (block_waves(tx_block<F
     double* red = cv.take<double>(BLK / 64);
     constexpr int TTS = FB ? tt_size(LOGN) : 0;
     C* tt = cv.take<C>(TTS);  // throughput kernel: inverse per-pass twiddles
+    // adaptive throughput kernel: per subcarrier (LUT offset << 8 | tx bit mask); unused
+    // subcarriers point at a zero entry appended to the LUT pool
+    uint32_t* sce = cv.take<uint32_t>(FB == 1 ? N : 0);
 
     if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
     // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element)
     const R lut_scale = scm ? (R)1 : (R)cm.scale;
     for (int i = threadIdx.x; i < cm.lut_len; i += BLK) lut[i] = cscale(((const C*)cm.lut)[i], lut_scale);
+    if constexpr (FB == 1) {
+        if (threadIdx.x == 0) lut[cm.lut_len] = mk<R>(0, 0);
+        for (int k = threadIdx.x; k < N; k += BLK) {
+            const ScInfo sc = cm.sc[k];
+            sce[k] = sc.lut < 0 ? (uint32_t)cm.lut_len << 8
+                                : ((uint32_t)cm.axis[sc.lut].lut_off << 8) | ((1u << sc.bits) - 1u);
+        }
+    }
     if (threadIdx.x < 32) {
         const C hq = threadIdx.x < L ? ((const C*)a.h)[threadIdx.x] : mk<R>(0, 0);
         h[threadIdx.x] = hq;
@@ -244,7 +263,18 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()), (block_waves(tx_block<F
             // map (QAMConstellationMapper.encode, constellation/models.py:240-246); the
             // 1/sqrt(N) of ifft(norm="ortho") folded in
             C x[E];
-            if constexpr (FB > 0) {
+            if constexpr (FB == 1) {
+                // element i: the low b_k bits of lane byte i through its subcarrier's LUT.  The
+                // table index is made opaque per symbol so the 16 loop-invariant reads are not
+                // hoisted out of the symbol loop as 16 live registers.
+                int st = t;
+                asm volatile("" : "+v"(st));
+                static_for<0, E>([&](auto I) {
+                    const uint32_t e = sce[st + I * TPS];
+                    const uint32_t v = (lane_word(tb.lane, I >> 2) >> (8 * (I & 3))) & e & 0xFFu;
+                    x[I] = active ? lut[(e >> 8) + v] : mk<R>(0, 0);
+                });
+            } else if constexpr (FB > 0) {
                 static_for<0, E>([&](auto I) { x[I] = active ? lut[tb.template fixed<I>()] : mk<R>(0, 0); });
             } else {
 #pragma unroll
@@ -335,11 +365,16 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()), (block_waves(tx_block<F
                 }
                 sym_sync<TPS>();
                 if (active && c >= 0) {
-                    f32x2 hv[LT], hs[LT];  // taps (zero past L), LDS broadcast reads
+                    // taps (zero past L), LDS broadcast reads; the opaque offset keeps the reads
+                    // in the symbol loop (hoisted, the 4 LT registers stay live through the FFT
+                    // and spill)
+                    int ho = 0;
+                    asm volatile("" : "+v"(ho));
+                    f32x2 hv[LT], hs[LT];
 #pragma unroll
                     for (int q = 0; q < LT; ++q) {
-                        hv[q] = f32x2{(float)h[q].re, (float)h[q].im};
-                        hs[q] = f32x2{(float)hsw[q].re, (float)hsw[q].im};
+                        hv[q] = f32x2{(float)h[ho + q].re, (float)h[ho + q].im};
+                        hs[q] = f32x2{(float)hsw[ho + q].re, (float)hsw[ho + q].im};
                     }
                     const C* wb = row + (A + (A >> 4) + 17 * t);
                     f32x2 win[WN];
@@ -462,10 +497,24 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     unsigned long long* redc = cv.take<unsigned long long>(BLK / 64);
     constexpr int TTS = FB ? tt_size(LOGN) : 0;
     C* tt = cv.take<C>(TTS);  // throughput kernel: forward per-pass twiddles
+    OrderParams* ordt = cv.take<OrderParams>(FB == 1 ? 8 : 0);  // adaptive: per-order slicer
 
     if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
+    if constexpr (FB == 1) {
+        if (threadIdx.x < 8) {
+            OrderParams o{0.f, 0.f, 0x4B400000u, 0u};  // unused subcarrier: level 0, no bits
+            if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
+                const AxisInfo ax = cm.axis[threadIdx.x];
+                o.mul = (float)(ax.inv_step * cm.scale);  // the FFT output stays unscaled
+                o.add = (float)(-ax.lev0 * ax.inv_step);
+                o.smax = 0x4B400000u + (uint32_t)(ax.side - 1);
+                o.meta = ((1u << ax.bits) - 1u) | ((1u << ax.hbits) << 8);
+            }
+            ordt[threadIdx.x] = o;
+        }
+    }
     __syncthreads();
 
     // a symbol group of >= 64 threads is whole wavefronts: make its index wave-uniform
@@ -478,11 +527,26 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     const int cp = cm.cp;
     const R scale = (R)cm.scale;
     Slicer<R> slicer;
-    PermSlicer<FB ? FB : 2> pslicer;
-    if constexpr (FB > 0)
+    PermSlicer<(FB > 1 ? FB : 2)> pslicer;
+    // adaptive throughput kernel: the LDS byte offset of each element's order entry, four
+    // elements per word (the lane's subcarriers do not change from symbol to symbol)
+    uint32_t ocode[FB == 1 ? E / 4 : 1];
+    if constexpr (FB == 1) {
+#pragma unroll
+        for (int q = 0; q < E / 4; ++q) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int lid = cm.sc[t + (4 * q + j) * TPS].lut;
+                w |= (uint32_t)(sizeof(OrderParams) * (lid < 0 ? kUnusedOrder : lid)) << (8 * j);
+            }
+            ocode[q] = w;
+        }
+    } else if constexpr (FB > 1) {
         pslicer.load(axis[0], (float)cm.scale);  // the FFT output stays unscaled
-    else if (!adaptive)
+    } else if (!adaptive) {
         slicer.load(axis[0]);
+    }
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     R sigma = 0;
@@ -593,7 +657,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
         }
         if (active && !(a.flags & 8)) {
             const int64_t sbit = sg * cm.bps;
-            const bool all_valid = FB > 0 || sbit + cm.bps <= a.n_valid_bits;
+            const bool all_valid = FB > 1 || sbit + cm.bps <= a.n_valid_bits;
             uint32_t bes = 0, ses = 0;
             auto equalized = [&](int i) {
                 const int k = t + i * TPS;
@@ -606,7 +670,39 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                 }
                 return v;
             };
-            if constexpr (FB > 0) {
+            if constexpr (FB == 1) {
+                // four elements per lane word, each through its subcarrier's order (the codes
+                // are made opaque per symbol: the order-table reads stay inside the loop)
+                static_for<0, E / 4>([&](auto Q) {
+                    constexpr int q = Q;
+                    C z[4];
+                    const OrderParams* op[4];
+                    uint32_t oc = ocode[q];
+                    asm volatile("" : "+v"(oc));
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        z[j] = equalized(4 * q + j);
+                        op[j] = (const OrderParams*)((const unsigned char*)ordt + ((oc >> (8 * j)) & 0xFFu));
+                    }
+                    uint32_t d = adaptive_diff(z, op, lane_word(tb.lane, q));
+                    ses += PermSlicer<8>::nonzero_bytes(d);
+                    if (!all_valid) {
+                        // a trailing partial byte of the run is not compared (constellation/
+                        // adaptive.py:259-263): keep the first bits (MSB first) of the valid range
+                        uint32_t vm = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const ScInfo sc = cm.sc[t + (4 * q + j) * TPS];
+                            if (sc.lut < 0) continue;
+                            const int64_t nvb = a.n_valid_bits - (sbit + sc.bitoff);
+                            const int keep = nvb <= 0 ? 0 : (nvb >= sc.bits ? sc.bits : (int)nvb);
+                            vm |= (((1u << keep) - 1u) << (sc.bits - keep)) << (8 * j);
+                        }
+                        d &= vm;
+                    }
+                    bes += __popc(d);
+                });
+            } else if constexpr (FB > 0) {
                 // four elements per lane word: slice, look up, compare, count
                 static_for<0, E / 4>([&](auto Q) {
                     constexpr int q = Q;
@@ -615,7 +711,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                     for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
                     const uint32_t d = pslicer.diff(z, lane_word(tb.lane, q));
                     bes += __popc(d);
-                    ses += PermSlicer<FB ? FB : 2>::nonzero_bytes(d);
+                    ses += PermSlicer<FB>::nonzero_bytes(d);
                 });
             } else {
 #pragma unroll

@@ -110,8 +110,8 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
         const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
         a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
     }
-    const size_t sm = smem_tx<R>(LOGN, BLK, a.c.lut_len, a.c.words_per_sym, a.L, a.slot, FB ? tt_size(LOGN) : 0,
-                                 FB > 0 && LT > 0);
+    const size_t sm = smem_tx<R>(LOGN, BLK, a.c.lut_len + (FB == 1), a.c.words_per_sym, a.L, a.slot,
+                                 FB ? tt_size(LOGN) : 0, FB > 0 && LT > 0, FB == 1 ? (size_t)4 << LOGN : 0);
     auto fn = k_tx<R, LOGN, FB, LT>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
@@ -136,10 +136,14 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
 }
 
 // Throughput configuration (complex64, fixed square QAM, Philox bits; N >= 64) -> the
-// kernel specialised on the bits per subcarrier; anything else -> the generic kernel.
+// kernel specialised on the bits per subcarrier; adaptive bit loading over the reference's
+// square-QAM LUTs -> the adaptive throughput kernel (FB = 1); anything else -> the generic
+// kernel.
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
+        if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
+            return tx_fast<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn) {
             switch (a.c.b) {
                 case 2: return tx_fast<R, LOGN, 2>(a, grid, s);
@@ -169,7 +173,8 @@ hipError_t launch_tx(int logn, const TxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN, int EQ, int FB>
 static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     constexpr int BLK = rx_block<FB, LOGN, EQ>();
-    const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym, FB ? tt_size(LOGN) : 0);
+    const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym, FB ? tt_size(LOGN) : 0,
+                                 FB == 1 ? 8 * sizeof(OrderParams) : 0);
     auto fn = k_rx<R, LOGN, EQ, FB>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
@@ -191,6 +196,9 @@ static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN>
 static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
+        if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
+            !a.c.scm && !a.c.zpad && !a.c.nn)
+            return rx_eq<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr && !a.c.scm &&
             !a.c.zpad && !a.c.nn) {
             switch (a.c.b) {

@@ -103,6 +103,7 @@ struct TxRxCommon {
     int scm, zpad, nn;
     int ystride;  // stored channel samples per OFDM symbol: N, or N + cp with zero padding
     const double* lut64;
+    int upat;  // every LUT has the reference's square-QAM level patterns (kUPat): adaptive fast path
 };
 
 struct TxArgs {
@@ -155,7 +156,8 @@ inline int tx_slot(int logn, int cp, int L) {
 // fused kernels, blk threads; tts = per-pass twiddle entries (throughput kernels) or 0
 // (the throughput kernels, tts > 0, carve no two-level twiddles and no staged bit words)
 template <typename R>
-inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int slot, int tts, bool wfir) {
+inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int slot, int tts, bool wfir,
+                      size_t extra = 0 /* adaptive throughput kernel: per-subcarrier table */) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn, blk);
     const int tls = L > 1 ? L - 1 : 1;
@@ -163,16 +165,17 @@ inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int slot, 
     return rnd16((tts > 0 ? 0 : 128) * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(wfir ? 32 * c : 0) +
            rnd16(4 * sizeof(AxisInfo)) +
            rnd16((size_t)spb * slot * c) + rnd16((size_t)spb * tls * c) +
-           rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(double)) + rnd16((size_t)tts * c);
+           rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(double)) + rnd16((size_t)tts * c) +
+           rnd16(extra);
 }
 template <typename R>
-inline size_t smem_rx(int logn, int blk, int wps, int tts) {
+inline size_t smem_rx(int logn, int blk, int wps, int tts, size_t extra = 0 /* adaptive: order table */) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn, blk);
     if (tts > 0) wps = 0;
     return rnd16((tts > 0 ? 0 : 128) * c) + rnd16(4 * sizeof(AxisInfo)) + rnd16((size_t)spb * geo_padn(logn) * c) +
            rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(R)) +
-           rnd16((size_t)(blk / 64) * sizeof(unsigned long long)) + rnd16((size_t)tts * c);
+           rnd16((size_t)(blk / 64) * sizeof(unsigned long long)) + rnd16((size_t)tts * c) + rnd16(extra);
 }
 
 // ---- launchers (instantiated for float and double in ofdm_kernels_f{32,64}.hip)
