@@ -180,7 +180,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 // stream samples of the previous symbol) is carried in LDS; the first symbol of a chunk
 // regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
 template <typename R, int LOGN, int FB, int LT>
-__global__ __launch_bounds__((tx_block<FB, LOGN, LT>()), (block_waves(tx_block<FB, LOGN, LT>(), OFDM_TX_WAVES))) void k_tx(
+__global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
+                             (block_waves(tx_block<FB, LOGN, LT>(),
+                                          FB > 0 && LT > 0 ? OFDM_TX_WFIR_WAVES : OFDM_TX_WAVES))) void k_tx(
     TxArgs a) {
     constexpr int BLK = tx_block<FB, LOGN, LT>();
     constexpr bool WFIR = FB > 0 && LT > 0;  // register window FIR
