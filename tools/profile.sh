@@ -6,7 +6,7 @@ tag=$1; shift
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 out=gpurun_out/prof_$tag
 mkdir -p $out
-args="--steps ${PROF_STEPS:-5} --warmup 1 --no-cpu-baseline $*"
+args="--steps ${PROF_STEPS:-5} --warmup 1 --no-cpu-baseline --no-ber-check $*"
 run() {  # name seconds rocprof-args...
     local name=$1 secs=$2; shift 2
     timeout -k 10 $secs rocprofv3 "$@" -d $out/$name -o $name --output-format csv -- python3 bench.py $args \
