@@ -105,6 +105,7 @@ struct ofdm_plan_s {
     std::map<void*, DevBuf> ws;
     int has_const, has_channel, separable, zp, single_carrier;
     int upat;  // all LUTs use the reference's square-QAM level -> index patterns (kUPat)
+    int psk_m; // the single LUT is the reference's M-PSK (LUT[gray(i)] = exp(2 pi j i / M)), M <= 32
     size_t csize() const { return prec == OFDM_F32 ? 8 : 16; }
 };
 
@@ -185,6 +186,18 @@ bool universal_patterns(const std::vector<AxisInfo>& axes) {
         }
     }
     return true;
+}
+
+// M if the LUT is the reference's M-PSK (constellation/models.py:356-380: LUT[gray(i)] =
+// exp(2 pi j i / M)) with 2 <= M <= 32, else 0.
+int psk_order(const double* lut, int m) {
+    if (m < 2 || m > 32 || (m & (m - 1))) return 0;
+    for (int i = 0; i < m; ++i) {
+        const int g = i ^ (i >> 1);
+        const double a = 2.0 * M_PI * i / m;
+        if (std::fabs(lut[2 * g] - std::cos(a)) > 1e-12 || std::fabs(lut[2 * g + 1] - std::sin(a)) > 1e-12) return 0;
+    }
+    return m;
 }
 
 // Diagnostic ablation switches for timing studies (tools/ablate.py); unset = 0 = normal run.
@@ -300,6 +313,7 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
         p->separable = 1;
         for (const AxisInfo& ax : axes) p->separable &= ax.side > 0;
         p->upat = p->separable && universal_patterns(axes);
+        p->psk_m = (!p->separable && d->n_luts == 1) ? psk_order(d->lut_pool, d->lut_orders[0]) : 0;
         std::vector<double> pool(d->lut_pool, d->lut_pool + 2 * off);
         if ((rc = upload_cpx(p->lut, pool, p->prec, s))) return rc;
         if ((rc = upload(p->lut64, pool.data(), pool.size(), s))) return rc;
@@ -644,6 +658,9 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
     c.ystride = c.zpad ? p->n + p->cp : p->n;
     c.lut64 = (const double*)p->lut64.p;
     c.upat = p->upat;
+    c.psk_m = p->prec == OFDM_F32 ? p->psk_m : 0;  // complex128 keeps the reference's hypot search
+    for (int q = 0; q < 4; ++q)
+        c.psk_tan[q] = (c.psk_m >= 8 && q < c.psk_m / 8) ? (float)std::tan((q + 0.5) * 2.0 * M_PI / c.psk_m) : 0.f;
 }
 
 int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int64_t sym0, int64_t n_sym,

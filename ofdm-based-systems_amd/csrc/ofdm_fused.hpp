@@ -144,14 +144,43 @@ struct TxBits {
     }
 };
 
+// M-PSK as the reference builds it (constellation/models.py:356-380: LUT[gray(i)] =
+// exp(2 pi j i / M)), complex64: the nearest point is the nearest angle, found without a
+// search.  The point is folded into the first octant (|x|, |y|, swap when |y| > |x|), the
+// sector inside the octant is counted against tan((q + 1/2) 2 pi / M) for q < M/8, and the
+// three reflections are undone on the sector index k; the LUT index is gray(k).  M = 2 and
+// 4 have no in-octant boundaries.  Decisions differ from the brute-force search only on a
+// decision boundary (|y| = |x| or an exact tangent), a probability-zero event under noise.
+__device__ __forceinline__ uint32_t psk_decide(cpx<float> v, const TxRxCommon& cm) {
+    const int M = cm.psk_m;
+    const float ax = fabsf(v.re), ay = fabsf(v.im);
+    const bool sw = ay > ax, sx = v.re < 0.f, sy = v.im < 0.f;
+    const float u = fmaxf(ax, ay), w = fminf(ax, ay);  // angle of (u, w) in [0, pi/4]
+    int k;
+    if (M == 2) {
+        k = sx ? 1 : 0;
+    } else {
+        int q = 0;
+        for (int j = 0; j < (M >> 3); ++j) q += w > cm.psk_tan[j] * u;
+        const int quarter = M >> 2;
+        int k1 = sw ? quarter - q : q;        // reflect about 45 degrees
+        if (M == 4) k1 = sw ? 1 : 0;
+        int k2 = sx ? 2 * quarter - k1 : k1;  // reflect about 90 degrees
+        k = sy ? (M - k2) & (M - 1) : k2;     // reflect about 0 degrees
+    }
+    return (uint32_t)(k ^ (k >> 1));
+}
+
 // Nearest constellation point of a non-separable LUT (PSK).  complex128: the reference's
 // |z - C_m| with hypot and the first index on ties (nn_index); complex64 (throughput
-// mode): squared distances in float against the plan-precision LUT.
+// mode): the sector decision above for the reference's M-PSK, else squared distances in
+// float against the plan-precision LUT.
 template <typename R>
 __device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm) {
     if constexpr (sizeof(R) == 8) {
         return (uint32_t)nn_index(v.re, v.im, cm.lut64, cm.lut_len);
     } else {
+        if (cm.psk_m > 0) return psk_decide(v, cm);
         const cpx<float>* L = (const cpx<float>*)cm.lut;
         float bd = INFINITY;
         uint32_t best = 0;

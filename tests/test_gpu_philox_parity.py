@@ -49,6 +49,11 @@ CASES = [
     (256, 8, "Lin-Phoong_P1", "MMSE", 512, 17.0, B.OFDM_F32, {"scheme": "PSK"}),
     (128, 4, "Lin-Phoong_P2", "MMSE", 1024, 10.0, B.OFDM_F64, {"modulator": "SC", "prefix": "ZP", "scheme": "PSK"}),
     (2048, 16, "Lin-Phoong_P1", "MMSE", 128, 19.0, B.OFDM_F32, {"prefix": "ZP", "modulator": "SC"}),
+    # complex64 M-PSK: sector decisions (octant fold + tangent thresholds) vs the oracle's search
+    (64, 2, "two_ray", "ZF", 2048, 4.0, B.OFDM_F32, {"scheme": "PSK"}),
+    (128, 4, "severe_multipath", "MMSE", 1024, 8.0, B.OFDM_F32, {"scheme": "PSK"}),
+    (1024, 16, "severe_multipath", "MMSE", 128, 16.0, B.OFDM_F32, {"scheme": "PSK"}),
+    (512, 32, "Lin-Phoong_P1", "ZF", 128, 22.0, B.OFDM_F32, {"scheme": "PSK"}),
     # CAPACITY_BASED bit loading (config d): per-subcarrier orders from water-filling at the SNR;
     # an odd symbol count leaves a trailing partial byte that is not compared
     (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F32, {"adaptive": True}),
