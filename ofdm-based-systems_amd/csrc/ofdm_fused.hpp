@@ -222,7 +222,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
     const bool adaptive = FB ? false : (bool)cm.adaptive;
     // generic kernel variants: single-carrier OFDM (no IFFT, modulation/models.py:
     // 58-70) and the zero-padding guard (prefix/models.py:55-67: [x | 0 ... 0])
-    const bool scm = FB ? false : (bool)cm.scm;
+    const bool scm = FB == 1 ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
     const bool zp = FB ? false : (bool)cm.zpad;
     const int ystride = FB ? N : cm.ystride;  // stored samples per OFDM symbol: N, or N + cp (ZP)
     const int cp = cm.cp, L = LT != 0 ? a.L : 1;
@@ -515,7 +515,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     // generic kernel variants: single-carrier OFDM (FFT -> equalise -> IFFT,
     // modulation/models.py:72-91), zero-padding guard (overlap-add, prefix/models.py:69-101)
     // and non-separable constellations (PSK: brute-force nearest point, constellation/models.py:19-27)
-    const bool scm = FB ? false : (bool)cm.scm;
+    const bool scm = FB == 1 ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
     const bool zp = FB ? false : (bool)cm.zpad;
     const bool nn = FB ? false : (bool)cm.nn;
     const int ystride = FB ? N : cm.ystride;
@@ -527,11 +527,13 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     R* red = cv.take<R>(BLK / 64);
     unsigned long long* redc = cv.take<unsigned long long>(BLK / 64);
     constexpr int TTS = FB ? tt_size(LOGN) : 0;
-    C* tt = cv.take<C>(TTS);  // throughput kernel: forward per-pass twiddles
+    // throughput kernel: forward per-pass twiddles, plus the inverse ones for SC-OFDM's IFFT
+    const int tts_all = FB > 1 && scm ? 2 * TTS : TTS;
+    C* tt = cv.take<C>(tts_all);
     OrderParams* ordt = cv.take<OrderParams>(FB == 1 ? 8 : 0);  // adaptive: per-order slicer
 
     if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
-    for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
+    for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     if constexpr (FB == 1) {
         if (threadIdx.x < 8) {
@@ -574,7 +576,8 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
             ocode[q] = w;
         }
     } else if constexpr (FB > 1) {
-        pslicer.load(axis[0], (float)cm.scale);  // the FFT output stays unscaled
+        // the FFT output stays unscaled (x sqrt N); SC-OFDM adds the unscaled IFFT (x sqrt N)
+        pslicer.load(axis[0], (float)(scm ? cm.scale * cm.scale : cm.scale));
     } else if (!adaptive) {
         slicer.load(axis[0]);
     }
@@ -682,9 +685,13 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                     x[i] = cmul(x[i], mmse_coef<R>(eqa[k], eqb[k], nv));
             }
             sym_sync<TPS>();  // the forward FFT has read the row
-            fft_reg<R, LOGN, true, false>(x, row, tw, tw + 64, t, tt);
+            if constexpr (FB > 1) {
+                fft_reg<R, LOGN, true, true>(x, row, tw, tw + 64, t, tt + TTS);  // 1/N in the slicer
+            } else {
+                fft_reg<R, LOGN, true, false>(x, row, tw, tw + 64, t, tt);
 #pragma unroll
-            for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
+                for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
+            }
         }
         if (active && !(a.flags & 8)) {
             const int64_t sbit = sg * cm.bps;

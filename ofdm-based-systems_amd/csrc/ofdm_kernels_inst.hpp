@@ -144,7 +144,7 @@ static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
             return tx_fast<R, LOGN, 1>(a, grid, s);
-        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn) {
+        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.zpad && !a.c.nn) {  // OFDM or SC-OFDM
             switch (a.c.b) {
                 case 2: return tx_fast<R, LOGN, 2>(a, grid, s);
                 case 4: return tx_fast<R, LOGN, 4>(a, grid, s);
@@ -173,7 +173,7 @@ hipError_t launch_tx(int logn, const TxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN, int EQ, int FB>
 static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     constexpr int BLK = rx_block<FB, LOGN, EQ>();
-    const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym, FB ? tt_size(LOGN) : 0,
+    const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym, FB ? tt_size(LOGN) * (FB > 1 && a.c.scm ? 2 : 1) : 0,
                                  FB == 1 ? 8 * sizeof(OrderParams) : 0);
     auto fn = k_rx<R, LOGN, EQ, FB>;
     hipError_t e = set_smem(fn, sm);
@@ -199,8 +199,8 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
             !a.c.scm && !a.c.zpad && !a.c.nn)
             return rx_eq<R, LOGN, 1>(a, grid, s);
-        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr && !a.c.scm &&
-            !a.c.zpad && !a.c.nn) {
+        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
+            !a.c.zpad && !a.c.nn) {  // OFDM or SC-OFDM
             switch (a.c.b) {
                 case 2: return rx_eq<R, LOGN, 2>(a, grid, s);
                 case 4: return rx_eq<R, LOGN, 4>(a, grid, s);

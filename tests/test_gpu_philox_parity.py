@@ -49,6 +49,9 @@ CASES = [
     (256, 8, "Lin-Phoong_P1", "MMSE", 512, 17.0, B.OFDM_F32, {"scheme": "PSK"}),
     (128, 4, "Lin-Phoong_P2", "MMSE", 1024, 10.0, B.OFDM_F64, {"modulator": "SC", "prefix": "ZP", "scheme": "PSK"}),
     (2048, 16, "Lin-Phoong_P1", "MMSE", 128, 19.0, B.OFDM_F32, {"prefix": "ZP", "modulator": "SC"}),
+    # SC-OFDM on the throughput kernels (FFT -> EQ -> IFFT with the per-pass tables)
+    (1024, 64, "severe_multipath", "MMSE", 256, 20.0, B.OFDM_F32, {"modulator": "SC"}),
+    (256, 16, "flat_fading", "NONE", 1024, 12.0, B.OFDM_F32, {"modulator": "SC"}),
     # complex64 M-PSK: sector decisions (octant fold + tangent thresholds) vs the oracle's search
     (64, 2, "two_ray", "ZF", 2048, 4.0, B.OFDM_F32, {"scheme": "PSK"}),
     (128, 4, "severe_multipath", "MMSE", 1024, 8.0, B.OFDM_F32, {"scheme": "PSK"}),
