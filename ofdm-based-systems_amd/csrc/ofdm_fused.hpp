@@ -223,8 +223,12 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
     // generic kernel variants: single-carrier OFDM (no IFFT, modulation/models.py:
     // 58-70) and the zero-padding guard (prefix/models.py:55-67: [x | 0 ... 0])
     const bool scm = FB == 1 ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
-    const bool zp = FB ? false : (bool)cm.zpad;
-    const int ystride = FB ? N : cm.ystride;  // stored samples per OFDM symbol: N, or N + cp (ZP)
+    // zero-padding guard (run-time, uniform); compiled out of the flat throughput TX (a zero
+    // guard needs cp > 0, the launcher sends it to the LT = -1 kernel), where the run-time
+    // row stride alone cost 15 % (config b TX 1.64 -> 1.92 ms)
+    constexpr bool ZP_OK = !(FB == 1 || (FB > 1 && LT == 0));
+    const bool zp = ZP_OK ? (bool)cm.zpad : false;
+    const int ystride = ZP_OK ? cm.ystride : N;  // stored samples per OFDM symbol: N, or N + cp (ZP)
     const int cp = cm.cp, L = LT != 0 ? a.L : 1;
     const int slot = a.slot;  // complex elements per symbol row (>= PADN and >= L-1+cp+N)
     const int tls = L > 1 ? L - 1 : 1;
@@ -516,9 +520,9 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     // modulation/models.py:72-91), zero-padding guard (overlap-add, prefix/models.py:69-101)
     // and non-separable constellations (PSK: brute-force nearest point, constellation/models.py:19-27)
     const bool scm = FB == 1 ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
-    const bool zp = FB ? false : (bool)cm.zpad;
+    const bool zp = FB == 1 ? false : (bool)cm.zpad;  // zero-padding guard (run-time, uniform)
     const bool nn = FB ? false : (bool)cm.nn;
-    const int ystride = FB ? N : cm.ystride;
+    const int ystride = FB == 1 ? N : cm.ystride;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
     AxisInfo* axis = cv.take<AxisInfo>(4);

@@ -125,9 +125,9 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
 template <typename R, int LOGN, int FB>
 static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     constexpr int TPS = Geo<LOGN>::TPS;
-    if (a.L == 1) return tx_launch<R, LOGN, FB, 0>(a, grid, s);
+    if (a.L == 1 && !a.c.zpad) return tx_launch<R, LOGN, FB, 0>(a, grid, s);
     if constexpr (LOGN >= 8) {
-        if (a.c.cp <= TPS) {
+        if (a.c.cp <= TPS && !a.c.zpad) {  // the register window assumes a cyclic prefix
             if (a.L <= 4) return tx_launch<R, LOGN, FB, 4>(a, grid, s);
             if (a.L <= 8) return tx_launch<R, LOGN, FB, 8>(a, grid, s);
         }
@@ -144,7 +144,7 @@ static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
             return tx_fast<R, LOGN, 1>(a, grid, s);
-        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.zpad && !a.c.nn) {  // OFDM or SC-OFDM
+        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.nn) {  // OFDM or SC-OFDM, CP or ZP
             switch (a.c.b) {
                 case 2: return tx_fast<R, LOGN, 2>(a, grid, s);
                 case 4: return tx_fast<R, LOGN, 4>(a, grid, s);
@@ -200,7 +200,7 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
             !a.c.scm && !a.c.zpad && !a.c.nn)
             return rx_eq<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
-            !a.c.zpad && !a.c.nn) {  // OFDM or SC-OFDM
+            !a.c.nn) {  // OFDM or SC-OFDM, CP or ZP
             switch (a.c.b) {
                 case 2: return rx_eq<R, LOGN, 2>(a, grid, s);
                 case 4: return rx_eq<R, LOGN, 4>(a, grid, s);
