@@ -10,10 +10,11 @@
 // workgroup run decoupled.
 //
 // Specialisations: FB = 2/4/6/8 selects the throughput kernel (fixed square QAM with
-// b = FB bits, Philox-keyed bits and noise, complex64) with everything else compiled
-// out; FB = 1 is the throughput kernel for adaptive bit loading (per-subcarrier square-QAM
-// orders, CAPACITY_BASED); FB = 0 is the generic kernel (reference-mode bytes and normals,
-// SC-OFDM, zero padding, PSK, complex128).
+// b = FB bits, Philox-keyed bits and noise, complex64; OFDM or SC-OFDM, cyclic prefix or
+// zero padding as wave-uniform run-time flags); FB = 1 is the throughput kernel for adaptive
+// bit loading (per-subcarrier square-QAM orders, CAPACITY_BASED, OFDM with a cyclic prefix);
+// FB = 0 is the generic kernel (reference-mode bytes and normals, PSK, complex128, adaptive
+// SC-OFDM / zero padding).
 #pragma once
 
 #include <type_traits>

@@ -135,10 +135,10 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     return tx_launch<R, LOGN, FB, -1>(a, grid, s);
 }
 
-// Throughput configuration (complex64, fixed square QAM, Philox bits; N >= 64) -> the
-// kernel specialised on the bits per subcarrier; adaptive bit loading over the reference's
-// square-QAM LUTs -> the adaptive throughput kernel (FB = 1); anything else -> the generic
-// kernel.
+// Throughput configuration (complex64, fixed square QAM, Philox bits; N >= 64; OFDM or
+// SC-OFDM, cyclic prefix or zero padding) -> the kernel specialised on the bits per
+// subcarrier; adaptive bit loading over the reference's square-QAM LUTs (OFDM, cyclic
+// prefix) -> the adaptive throughput kernel (FB = 1); anything else -> the generic kernel.
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
