@@ -752,7 +752,17 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                     C z[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
-                    const uint32_t d = pslicer.diff(z, lane_word(tb.lane, q));
+                    uint32_t d;
+                    // the reference's M-PSK (M <= 32 with even b: 4- and 16-PSK): sector
+                    // decisions (psk_decide); compiled out of the 64/256-QAM kernels
+                    if (FB <= 4 && cm.psk_m > 0) {
+                        uint32_t r = 0;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) r |= psk_decide(z[j], cm) << (8 * j);
+                        d = r ^ (lane_word(tb.lane, q) & PermSlicer<FB>::BYTE_MASK);
+                    } else {
+                        d = pslicer.diff(z, lane_word(tb.lane, q));
+                    }
                     bes += __popc(d);
                     ses += PermSlicer<FB>::nonzero_bytes(d);
                 });

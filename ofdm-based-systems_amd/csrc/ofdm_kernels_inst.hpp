@@ -144,7 +144,7 @@ static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
             return tx_fast<R, LOGN, 1>(a, grid, s);
-        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.nn) {  // OFDM or SC-OFDM, CP or ZP
+        if (!a.c.adaptive && a.c.bits == nullptr && (!a.c.nn || a.c.psk_m > 0)) {  // OFDM / SC, CP / ZP, QAM / PSK
             switch (a.c.b) {
                 case 2: return tx_fast<R, LOGN, 2>(a, grid, s);
                 case 4: return tx_fast<R, LOGN, 4>(a, grid, s);
@@ -200,7 +200,7 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
             !a.c.scm && !a.c.zpad && !a.c.nn)
             return rx_eq<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
-            !a.c.nn) {  // OFDM or SC-OFDM, CP or ZP
+            (!a.c.nn || a.c.psk_m > 0)) {  // OFDM / SC, CP / ZP, QAM / PSK
             switch (a.c.b) {
                 case 2: return rx_eq<R, LOGN, 2>(a, grid, s);
                 case 4: return rx_eq<R, LOGN, 4>(a, grid, s);
