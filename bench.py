@@ -225,7 +225,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "c64 (f32)" if prec == B.OFDM_F32 else "c128 (f64)",
-        "data": "synthetic: Philox4x32-10 bits and Box-Muller AWGN generated on the GPU per (seed, symbol)",
+        "data": "synthetic: Philox4x32-10 / MWC64X bits and Box-Muller AWGN (64-point phase table) generated "
+                "on the GPU per (seed, symbol)",
         "config": {
             "workload": f"{desc}; {per_gpu} OFDM symbols per GPU per step",
             "n_fft": N, "qam_order": M, "cp": cp, "channel": ch, "equalizer": eq_name, "snr_db": snr,

@@ -658,7 +658,9 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
     c.ystride = c.zpad ? p->n + p->cp : p->n;
     c.lut64 = (const double*)p->lut64.p;
     c.upat = p->upat;
-    c.psk_m = p->prec == OFDM_F32 ? p->psk_m : 0;  // complex128 keeps the reference's hypot search
+    // sector decisions for the reference's M-PSK in throughput mode (complex64, device bits) only:
+    // complex128 and the reference-stream mode keep the reference's nearest-point search
+    c.psk_m = (p->prec == OFDM_F32 && bits == nullptr) ? p->psk_m : 0;
     for (int q = 0; q < 4; ++q)
         c.psk_tan[q] = (c.psk_m >= 8 && q < c.psk_m / 8) ? (float)std::tan((q + 0.5) * 2.0 * M_PI / c.psk_m) : 0.f;
 }

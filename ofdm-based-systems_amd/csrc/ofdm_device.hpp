@@ -683,18 +683,31 @@ struct u4 {
     uint32_t x, y, z, w;
 };
 
+// a ^ b ^ k in one v_bitop3_b32 (truth table 0x96); k wave-uniform.  The compiler emits
+// two v_xor_b32 for the expression.
+__device__ __forceinline__ uint32_t xor3_s(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
 __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
     // keep the key schedule in the loop (SALU adds next to the VALU rounds): hoisted out of
     // a symbol loop it is 20 live SGPRs and spills
     asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        // one v_mad_u64_u32 per 32x32->64 product
+        // one v_mad_u64_u32 per 32x32->64 product, one v_bitop3 per three-way xor
         const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
         u4 n;
-        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        if (i == 0) {  // round 0: c.y, c.w are wave-uniform (symbol index, stream id)
+            n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+            n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        } else {
+            n.x = xor3_s((uint32_t)(p1 >> 32), c.y, k0);
+            n.z = xor3_s((uint32_t)(p0 >> 32), c.w, k1);
+        }
         n.y = (uint32_t)p1;
-        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
         n.w = (uint32_t)p0;
         c = n;
         k0 += 0x9E3779B9u;
@@ -704,12 +717,14 @@ __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 }
 
 // ------------------------------------------------------------------ throughput-mode streams
-// Definition (philox mode): thread t of OFDM symbol s owns elements k = t + TPS*i.  Its
-// lane generator is SFC32 seeded with words 0..2 of one Philox4x32-10 block, key = seed,
-// counter = (t, s mod 2^32, s >> 32, kLane).  Outputs 0..3 are the lane's 128 payload
-// bits (element i takes the low b_k bits of byte i, see lane_bits); outputs 4+3j, 5+3j,
-// 6+3j give the complex noise of elements 2j, 2j+1 (Sfc32::add_noise2).  Everything depends only on
-// (seed, s, N), so results do not depend on how symbols are batched or sharded.
+// Definition (philox mode, stream version 2): thread t of OFDM symbol s owns elements
+// k = t + TPS*i.  One Philox4x32-10 block per lane, key = seed, counter = (t, s mod 2^32,
+// s >> 32, kLane), gives words P0..P3.  The lane's 128 payload bits are the words
+// (P2, P3, m0, m1) (element i takes the low b_k bits of byte i, see lane_bits), where m0, m1,
+// ... are the outputs of an MWC64X generator seeded with x = P0, c = (P1 >> 1) | 1.  Output
+// m(2 + i) is the complex noise of element i (Mwc64x::noise): the radius from the word with
+// bits 3..8 set, the phase from bits 3..8 through a 64-entry table.  Everything depends only
+// on (seed, s, N), so results do not depend on how symbols are batched or sharded.
 constexpr uint32_t kLane = 0x1A7E5EEDu;
 
 __device__ __forceinline__ u4 philox_lane(uint64_t seed, int64_t s, uint32_t t, uint32_t stream) {
@@ -731,48 +746,64 @@ __device__ __forceinline__ uint32_t lane_bits(const u4& w, int i, int b) {
     return (lane_word(w, i >> 2) >> (8 * (i & 3))) & ((1u << b) - 1u);
 }
 
-// SFC32 (Doty-Humphrey's small fast counting generator): 96-bit state plus a counter,
-// 6 ALU ops per output.  The counter is the draw index, a compile-time constant in the
-// unrolled lane loops, so it costs nothing; the state comes from a Philox block.
-struct Sfc32 {
-    uint32_t a, b, c, n;
-    __device__ __forceinline__ void seed(const u4& v) {
-        a = v.x;
-        b = v.y;
-        c = v.z;
-        n = 0u;
+// Noise phase table: kNoisePhases points e^{2 pi i (j + 1/2) / 64} scaled by
+// sigma sqrt(2 ln 2) (float32), one per workgroup in LDS; entry j lives at byte 8 j, so a
+// word's bits 3..8 are its byte offset.  A uniform phase taken on 64 points leaves the
+// noise's projection on any direction Gaussian to within the trapezoid rule's error on
+// the smooth periodic tail integrand: P(Re(n e^{-i phi}) > d sigma) is off by < 2e-6 relative
+// for every phi and d >= 1, < 1e-10 at d >= 3 (tests/test_oracle_philox.py).
+constexpr int kNoisePhases = 64;
+constexpr uint32_t kNoisePhaseMask = 0x1F8u;      // bits 3..8: byte offset of entry j
+constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2)
+
+// MWC64X (D. B. Thomas, multiply-with-carry, base 2^32, A = 4294883355): state (x, c),
+// output x ^ c, then (c, x) <- hi/lo of A x + c -- one v_mad_u64_u32 (plus the move of the
+// carry into the addend pair and the xor) per 32-bit output.  Seeded from one Philox block:
+// c = (P1 >> 1) | 1 < A, so the state is never one of the two fixed points.
+constexpr uint32_t kMwcA = 4294883355u;
+struct Mwc64x {
+    uint32_t x, c;
+    __device__ __forceinline__ void seed(uint32_t p0, uint32_t p1) {
+        x = p0;
+        c = (p1 >> 1) | 1u;
     }
     __device__ __forceinline__ uint32_t next() {
-        const uint32_t r = a + b + (++n);
-        a = b ^ (b >> 9);
-        b = c + (c << 3);
-        c = ((c << 21) | (c >> 11)) + r;
+        const uint32_t r = x ^ c;
+        const uint64_t v = (uint64_t)kMwcA * x + c;
+        x = (uint32_t)v;
+        c = (uint32_t)(v >> 32);
         return r;
     }
-    // Two complex normals with per-component standard deviation sigma added to x0, x1, by
-    // Box-Muller on the hardware transcendentals (v_log_f32 = log2, v_sin/cos_f32 take
-    // revolutions): three outputs -- radius words u0, u1 (32 bits each, so the Rayleigh
-    // tail is exact to 6.7 sigma) and one angle word a giving the two phases
-    // v0 = (a >> 9) 2^-23 (bits 9..31) and v1 = (a & 0xffff) 2^-16.
-    // x += sigma sqrt(-2 ln u) (cos 2 pi v, sin 2 pi v), u = (u32 + 1/2) 2^-32 in (0, 1).
-    // Issue-count details: -2 ln2 sigma^2 log2(u) = m2s2ln2 log2(u32 + 1/2) + c32 (one FMA,
-    // c32 = -32 m2s2ln2; |.| in the sqrt source modifier absorbs a rounding-negative
-    // argument at u -> 1), and 1 + v0 is built as a float by one v_alignbit_b32 (sin and cos
-    // have period 1 in revolutions).
-    __device__ __forceinline__ void add_noise2(f32x2& x0, f32x2& x1, float m2s2ln2 /* -2 ln2 sigma^2 */,
-                                               float c32 /* -32 m2s2ln2 */) {
-        const float k16 = 1.52587890625e-05f;  // 2^-16
-        const uint32_t w0 = next(), w1 = next(), wa = next();
-        const float r0 = __builtin_amdgcn_sqrtf(
-            __builtin_fabsf(__builtin_fmaf(m2s2ln2, __builtin_amdgcn_logf((float)w0 + 0.5f), c32)));
-        const float r1 = __builtin_amdgcn_sqrtf(
-            __builtin_fabsf(__builtin_fmaf(m2s2ln2, __builtin_amdgcn_logf((float)w1 + 0.5f), c32)));
-        const float v0 = __uint_as_float(__builtin_amdgcn_alignbit(0x7Fu, wa, 9));  // 1 + v0
-        const float v1 = (float)(wa & 0xFFFFu) * k16;
-        x0 = __builtin_elementwise_fma(f32x2{__builtin_amdgcn_cosf(v0), __builtin_amdgcn_sinf(v0)}, f32x2{r0, r0}, x0);
-        x1 = __builtin_elementwise_fma(f32x2{__builtin_amdgcn_cosf(v1), __builtin_amdgcn_sinf(v1)}, f32x2{r1, r1}, x1);
+    // One complex normal with per-component standard deviation sigma added to x, from one
+    // output w by Box-Muller: u = float(w | 0x1F8) 2^-32 in (1.2e-7, 1] (the radius tail is
+    // exact to 5.6 sigma), radius sigma sqrt(-2 ln u) = sigma sqrt(2 ln 2) sqrt(32 - log2(w | 0x1F8))
+    // on the hardware v_log_f32 (log2) / v_sqrt_f32, phase from bits 3..8 through ntab (already
+    // holding sigma sqrt(2 ln 2)).  Bits 3..8 are forced to 1 in the radius word, so radius and
+    // phase come from disjoint bits.
+    __device__ __forceinline__ static f32x2 sample(uint32_t w, const f32x2* ntab, float& r) {
+        r = __builtin_amdgcn_sqrtf(32.0f - __builtin_amdgcn_logf((float)(w | kNoisePhaseMask)));
+        return *(const f32x2*)((const unsigned char*)ntab + (w & kNoisePhaseMask));
+    }
+    __device__ __forceinline__ void add_noise(f32x2& x0, const f32x2* ntab) {
+        float r;
+        const f32x2 e = sample(next(), ntab, r);
+        x0 = __builtin_elementwise_fma(f32x2{r, r}, e, x0);
+    }
+    __device__ __forceinline__ f32x2 noise(const f32x2* ntab) {
+        float r;
+        const f32x2 e = sample(next(), ntab, r);
+        return f32x2{r, r} * e;
     }
 };
+
+// Build the noise phase table in LDS (threads < 64; caller syncs).
+__device__ __forceinline__ void build_noise_table(f32x2* ntab, double sigma) {
+    if (threadIdx.x < kNoisePhases) {
+        const float s = (float)(sigma * kSqrt2Ln2);
+        const double th = (2.0 * threadIdx.x + 1.0) / kNoisePhases;  // (j + 1/2) / 32 half-turns
+        ntab[threadIdx.x] = f32x2{s * (float)cospi(th), s * (float)sinpi(th)};
+    }
+}
 
 // ------------------------------------------------------------------ constellation tables
 template <typename R>

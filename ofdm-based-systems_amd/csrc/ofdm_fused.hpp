@@ -35,6 +35,12 @@
 #ifndef OFDM_RX_WAVES
 #define OFDM_RX_WAVES 1
 #endif
+// RX order of the per-symbol prologue: 0 = Philox, loads, noise added element by element as the
+// loads land; 1 = loads, Philox, the whole noise into registers, then the adds; 2 = loads,
+// Philox, noise added element by element
+#ifndef OFDM_RX_NOISE_FIRST
+#define OFDM_RX_NOISE_FIRST 0
+#endif
 // Workgroup of the throughput (FB > 0) kernels at N <= 1024 (TX; RX without equaliser):
 // 8 waves share one copy of the twiddle tables and two workgroups fit the 160 KB LDS, i.e.
 // 4 waves per SIMD (register budget 128).  Other variants: 256 threads, OFDM_*_WAVES.
@@ -110,15 +116,17 @@ __device__ __forceinline__ cpx<R> mmse_coef(cpx<R> hc, R h2, R nv) {
 template <int FB, int TPS>
 struct TxBits {
     u4 lane;
-    Sfc32 g;
+    Mwc64x g;
     const uint32_t* W;
     int base_bit;
     bool from_words;
 
+    // payload words (P2, P3, m0, m1); the generator continues into the lane's noise
     __device__ __forceinline__ void seed_lane(uint64_t seed, int64_t s, int t) {
-        g.seed(philox_lane(seed, s, (uint32_t)t, kLane));
-        lane.x = g.next();
-        lane.y = g.next();
+        const u4 p = philox_lane(seed, s, (uint32_t)t, kLane);
+        g.seed(p.x, p.y);
+        lane.x = p.z;
+        lane.y = p.w;
         lane.z = g.next();
         lane.w = g.next();
     }
@@ -173,9 +181,9 @@ __device__ __forceinline__ uint32_t psk_decide(cpx<float> v, const TxRxCommon& c
 }
 
 // Nearest constellation point of a non-separable LUT (PSK).  complex128: the reference's
-// |z - C_m| with hypot and the first index on ties (nn_index); complex64 (throughput
-// mode): the sector decision above for the reference's M-PSK, else squared distances in
-// float against the plan-precision LUT.
+// |z - C_m| with hypot and the first index on ties (nn_index); complex64: the sector
+// decision above for the reference's M-PSK in throughput mode (cm.psk_m > 0 only there,
+// ofdm_abi.hip fill_common), else squared distances in float against the plan-precision LUT.
 template <typename R>
 __device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm) {
     if constexpr (sizeof(R) == 8) {
@@ -235,7 +243,12 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
     const int tls = L > 1 ? L - 1 : 1;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
-    C* lut = cv.take<C>(cm.lut_len + (FB == 1));
+    // throughput kernels: the LUT in static LDS at a link-time address, so an element's LUT read
+    // is addressed by its index bits alone (2^FB entries; adaptive: the pool + a zero entry);
+    // generic kernel: dynamic
+    constexpr int LUT_STATIC = FB == 1 ? kMaxLut + 1 : (FB > 1 ? (1 << FB) : 1);
+    __shared__ C lut_s[LUT_STATIC];
+    C* lut = FB > 0 ? lut_s : cv.take<C>(cm.lut_len);
     C* h = cv.take<C>(32);
     C* hsw = cv.take<C>(WFIR ? 32 : 0);  // window FIR: the taps swizzled, (-im, re)
     AxisInfo* axis = cv.take<AxisInfo>(4);
@@ -251,9 +264,14 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
 
     if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
-    // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element)
+    // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element);
+    // flat throughput kernel: the channel tap too (y = h0 ifft(X) = ifft(h0 X)), so the
+    // symbol leaves the IFFT as the channel output
+    constexpr bool FOLD_H0 = FB > 0 && LT == 0;
     const R lut_scale = scm ? (R)1 : (R)cm.scale;
-    for (int i = threadIdx.x; i < cm.lut_len; i += BLK) lut[i] = cscale(((const C*)cm.lut)[i], lut_scale);
+    const C hf = FOLD_H0 ? ((const C*)a.h)[0] : mk<R>(1, 0);
+    for (int i = threadIdx.x; i < cm.lut_len; i += BLK)
+        lut[i] = cscale(FOLD_H0 ? cmul(hf, ((const C*)cm.lut)[i]) : ((const C*)cm.lut)[i], lut_scale);
     if constexpr (FB == 1) {
         if (threadIdx.x == 0) lut[cm.lut_len] = mk<R>(0, 0);
         for (int k = threadIdx.x; k < N; k += BLK) {
@@ -298,6 +316,8 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
             if (FB == 0) sym_sync<TPS>();  // staged words visible
             // map (QAMConstellationMapper.encode, constellation/models.py:240-246); the
             // 1/sqrt(N) of ifft(norm="ortho") folded in
+            // (throughput kernels: an inactive symbol maps its zero lane words -- nothing of it
+            // is stored or counted, and its tail is zeroed below)
             C x[E];
             if constexpr (FB == 1) {
                 // element i: the low b_k bits of lane byte i through its subcarrier's LUT.  The
@@ -308,10 +328,10 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
                 static_for<0, E>([&](auto I) {
                     const uint32_t e = sce[st + I * TPS];
                     const uint32_t v = (lane_word(tb.lane, I >> 2) >> (8 * (I & 3))) & e & 0xFFu;
-                    x[I] = active ? lut[(e >> 8) + v] : mk<R>(0, 0);
+                    x[I] = lut[(e >> 8) + v];
                 });
             } else if constexpr (FB > 0) {
-                static_for<0, E>([&](auto I) { x[I] = active ? lut[tb.template fixed<I>()] : mk<R>(0, 0); });
+                static_for<0, E>([&](auto I) { x[I] = lut[tb.template fixed<I>()]; });
             } else {
 #pragma unroll
                 for (int i = 0; i < E; ++i) {
@@ -364,12 +384,14 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
                     C* yo = yout + sl * ystride;
 #pragma unroll
                     for (int i = 0; i < E; ++i) {
-                        const C yv = cmul(h0, x[i]);
+                        const C yv = FOLD_H0 ? x[i] : cmul(h0, x[i]);
                         if (yout && !(a.flags & 4)) yo[t + i * TPS] = yv;
                     }
                     if (zp && yout)
                         for (int j = t; j < cp; j += TPS) yo[N + j] = mk<R>(0, 0);
-                    if constexpr (FB > 0) {
+                    if constexpr (FOLD_H0) {
+                        py += pxs;  // the statistics above were taken on y (x |h0|^2 fixed below)
+                    } else if constexpr (FB > 0) {
                         py += (double)(norm2(h0) * pxs);  // |y|^2 = |h0|^2 |x|^2 (complex64 mode)
                     } else {
                         R pys = 0;
@@ -495,6 +517,11 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
             }
         }
     }
+    if constexpr (FOLD_H0) {  // |x|^2 = |y|^2 / |h0|^2
+        const double ih2 = 1.0 / ((double)h0.re * (double)h0.re + (double)h0.im * (double)h0.im);
+        px *= ih2;
+        mx *= ih2;
+    }
     py = block_sum<double, BLK>(py, red);
     px = block_sum<double, BLK>(px, red);
     mx = block_max<double, BLK>(mx, red);
@@ -524,6 +551,9 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     const bool zp = FB == 1 ? false : (bool)cm.zpad;  // zero-padding guard (run-time, uniform)
     const bool nn = FB ? false : (bool)cm.nn;
     const int ystride = FB == 1 ? N : cm.ystride;
+    // noise phase table: static LDS at a link-time constant address, so a lane word's bits 3..8
+    // (its byte offset) address an entry with no add
+    __shared__ f32x2 ntab[kNoisePhases];
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
     AxisInfo* axis = cv.take<AxisInfo>(4);
@@ -537,6 +567,15 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     C* tt = cv.take<C>(tts_all);
     OrderParams* ordt = cv.take<OrderParams>(FB == 1 ? 8 : 0);  // adaptive: per-order slicer
 
+    // sigma from the whole-stream mean power (noise/models.py:13-22)
+    const bool noise = a.noise_on && !(a.flags & 1);
+    double sigma_d = 0;
+    if (noise) {
+        const double p = a.stats[0] / (double)a.total_samples;
+        sigma_d = sqrt((p / a.snr_lin) / 2.0);
+    }
+    const R sigma = (R)sigma_d;
+    build_noise_table(ntab, sigma_d);
     if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
@@ -581,19 +620,13 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
             ocode[q] = w;
         }
     } else if constexpr (FB > 1) {
-        // the FFT output stays unscaled (x sqrt N); SC-OFDM adds the unscaled IFFT (x sqrt N)
-        pslicer.load(axis[0], (float)(scm ? cm.scale * cm.scale : cm.scale));
+        // the FFT output stays unscaled (x sqrt N); SC-OFDM adds the unscaled IFFT (x sqrt N).
+        // The reference's 4/16-PSK (psk_m > 0) decide by sector and have no axis tables.
+        if (cm.psk_m == 0) pslicer.load(axis[0], (float)(scm ? cm.scale * cm.scale : cm.scale));
     } else if (!adaptive) {
         slicer.load(axis[0]);
     }
 
-    // sigma from the whole-stream mean power (noise/models.py:13-22)
-    R sigma = 0;
-    const bool noise = a.noise_on && !(a.flags & 1);
-    if (noise) {
-        const double p = a.stats[0] / (double)a.total_samples;
-        sigma = (R)sqrt((p / a.snr_lin) / 2.0);
-    }
     const bool array_noise = FB == 0 && a.nr != nullptr && noise;
     const int64_t niter = (cm.n_sym + G::SPB - 1) / G::SPB;
     unsigned long long be = 0, se = 0;
@@ -603,7 +636,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
         const int64_t sg = cm.sym0 + sl;
         const bool active = sl < cm.n_sym;
         TxBits<FB, TPS> tb;
-        tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
+        if (!OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
         // kept channel samples + AWGN; the 1/sqrt(N) of fft(norm="ortho") folded in
         const C* ys = (const C*)a.y + sl * ystride;
         C x[E];
@@ -614,9 +647,15 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
 #pragma unroll
             for (int i = 0; i < E; ++i) x[i] = mk<R>(0, 0);
         }
-        const float m2s2ln2 = -1.3862943611198906f * (float)sigma * (float)sigma;
-        const float c32 = -32.0f * m2s2ln2;
-        if (active && array_noise) {
+        if (OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
+        if (OFDM_RX_NOISE_FIRST == 1 && sizeof(R) == 4 && active && noise && !array_noise) {
+            // the lane's noise while the loads are in flight, then one add per element
+            f32x2 nz[E];
+#pragma unroll
+            for (int i = 0; i < E; ++i) nz[i] = tb.g.noise(ntab);
+#pragma unroll
+            for (int i = 0; i < E; ++i) x[i] = x[i] + mk<R>(nz[i].x, nz[i].y);
+        } else if (active && array_noise) {
             const double* nr = a.nr + sg * (N + cp) + (zp ? 0 : cp);
             const double* ni = a.ni + sg * (N + cp) + (zp ? 0 : cp);
 #pragma unroll
@@ -625,27 +664,20 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                 x[i].im += sigma * (R)ni[t + i * TPS];
             }
         } else if (active && noise) {
-            static_assert(E % 2 == 0 || E == 1, "noise pairs");
+            // one lane word per element (stream outputs m2 .. m(E+1))
 #pragma unroll
-            for (int i = 0; i + 1 < E; i += 2) {
+            for (int i = 0; i < E; ++i) {
                 if constexpr (sizeof(R) == 4) {
-                    tb.g.add_noise2(x[i].v, x[i + 1].v, m2s2ln2, c32);
+                    tb.g.add_noise(x[i].v, ntab);
                 } else {
-                    f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
-                    tb.g.add_noise2(n0, n1, m2s2ln2, c32);
-                    x[i] = x[i] + mk<R>((R)n0.x, (R)n0.y);
-                    x[i + 1] = x[i + 1] + mk<R>((R)n1.x, (R)n1.y);
+                    const f32x2 n = tb.g.noise(ntab);
+                    x[i] = x[i] + mk<R>((R)n.x, (R)n.y);
                 }
-            }
-            if constexpr (E == 1) {
-                f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
-                tb.g.add_noise2(n0, n1, m2s2ln2, c32);
-                x[0] = x[0] + mk<R>((R)n0.x, (R)n0.y);
             }
         }
         if (zp && active) {
             // zero guard: received sample N + k (k < cp) is added onto sample k, noise included
-            // (philox mode: one more lane draw per tail sample, after the elements' noise)
+            // (philox mode: one more lane word per tail sample, after the elements' noise)
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 const int k = t + i * TPS;
@@ -655,9 +687,8 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
                         v.re += sigma * (R)a.nr[sg * (N + cp) + N + k];
                         v.im += sigma * (R)a.ni[sg * (N + cp) + N + k];
                     } else if (noise) {
-                        f32x2 n0 = {0.f, 0.f}, n1 = {0.f, 0.f};
-                        tb.g.add_noise2(n0, n1, m2s2ln2, c32);
-                        v = v + mk<R>((R)n0.x, (R)n0.y);
+                        const f32x2 n = tb.g.noise(ntab);
+                        v = v + mk<R>((R)n.x, (R)n.y);
                     }
                     x[i] = x[i] + v;
                 }

@@ -110,7 +110,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
         const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
         a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
     }
-    const size_t sm = smem_tx<R>(LOGN, BLK, a.c.lut_len + (FB == 1), a.c.words_per_sym, a.L, a.slot,
+    const size_t sm = smem_tx<R>(LOGN, BLK, FB > 0 ? 0 : a.c.lut_len, a.c.words_per_sym, a.L, a.slot,
                                  FB ? tt_size(LOGN) : 0, FB > 0 && LT > 0, FB == 1 ? (size_t)4 << LOGN : 0);
     auto fn = k_tx<R, LOGN, FB, LT>;
     hipError_t e = set_smem(fn, sm);
@@ -135,8 +135,8 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     return tx_launch<R, LOGN, FB, -1>(a, grid, s);
 }
 
-// Throughput configuration (complex64, fixed square QAM, Philox bits; N >= 64; OFDM or
-// SC-OFDM, cyclic prefix or zero padding) -> the kernel specialised on the bits per
+// Throughput configuration (complex64, fixed square QAM or the reference's 4/16-PSK (psk_m > 0),
+// Philox bits; N >= 64; OFDM or SC-OFDM, cyclic prefix or zero padding) -> the kernel specialised on the bits per
 // subcarrier; adaptive bit loading over the reference's square-QAM LUTs (OFDM, cyclic
 // prefix) -> the adaptive throughput kernel (FB = 1); anything else -> the generic kernel.
 template <typename R, int LOGN>
@@ -190,9 +190,9 @@ static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
     return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB>(a, grid, s);
 }
 
-// Throughput configuration (complex64, fixed square QAM, Philox bits and noise, no
-// received-symbol tap; N >= 64) -> kernel specialised on bits and equaliser; anything
-// else -> the generic kernel.
+// Throughput configuration (complex64, fixed square QAM or the reference's 4/16-PSK (psk_m > 0),
+// Philox bits and noise, no received-symbol tap; N >= 64) -> kernel specialised on bits and
+// equaliser; anything else -> the generic kernel.
 template <typename R, int LOGN>
 static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {

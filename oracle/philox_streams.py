@@ -13,20 +13,25 @@ fused throughput kernels are checked against the oracle on identical bits and no
 Like ``ofdm_oracle`` it is the CHECKER: only ``tests/``, ``__graft_entry__.smoke()`` and
 ``bench.py``'s ``cpu_baseline`` leg may import it.
 
-Definition (one OFDM symbol s of N subcarriers, E = min(16, N) elements per lane,
-TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS for i < E):
+Definition (stream version 2; one OFDM symbol s of N subcarriers, E = min(16, N) elements
+per lane, TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS for i < E):
 
-* lane generator: SFC32 (a, b, c, counter starting at 1) seeded with words 0..2 of one
-  Philox4x32-10 block, key = (seed mod 2^32, seed >> 32), counter = (t, s mod 2^32,
-  s >> 32, 0x1A7E5EED);
-* payload: outputs 0..3 are 128 bits; element i takes the low b bits of byte i (byte i =
-  bits 8*(i & 3).. of output i >> 2); with adaptive bit loading b = b_k of its subcarrier
+* lane block: words P0..P3 of one Philox4x32-10 block, key = (seed mod 2^32, seed >> 32),
+  counter = (t, s mod 2^32, s >> 32, 0x1A7E5EED);
+* lane generator: MWC64X (D. B. Thomas: multiply-with-carry, base 2^32, A = 4294883355;
+  output x ^ c, then (c, x) <- hi / lo of A*x + c) seeded with x = P0, c = (P1 >> 1) | 1;
+  its outputs are m0, m1, ...;
+* payload: the 128 bits (P2, P3, m0, m1); element i takes the low b bits of byte i (byte i =
+  bits 8*(i & 3).. of word i >> 2); with adaptive bit loading b = b_k of its subcarrier
   (b_k = 0: the subcarrier is unused and carries 0+0j);
-* noise: outputs 4+3j, 5+3j, 6+3j give elements 2j, 2j+1: radius words u0, u1, angle word
-  a; element 2j+q gets sigma*sqrt(-2 ln((u_q + 0.5) 2^-32)) * exp(2 pi i v_q) with
-  v_0 = (a >> 9) 2^-23 (bits 9..31), v_1 = (a & 0xffff) 2^-16, added to the kept time
-  sample k.  (float32 arithmetic on the GPU; here the radius argument follows the same
-  float32 rounding of u32 + 0.5 and the rest is evaluated in float64.)
+* noise: element i gets the complex normal of word w = m(2 + i), added to the kept time
+  sample k: radius sqrt(32 - log2(float32(w | 0x1F8))) (i.e. sqrt(-2 ln u) / sqrt(2 ln 2) with
+  u = (w | 0x1F8) 2^-32), times table entry j = (w >> 3) & 63, where entry j is
+  float32(sigma sqrt(2 ln 2)) * float32(cos, sin)(2 pi (j + 1/2) / 64) in float32.  (float32
+  arithmetic on the GPU, with the hardware log2 / sqrt; here the radius argument follows the
+  same float32 rounding of the word and the rest is evaluated in float64.)
+* zero padding: after the elements' noise a lane draws one more word per received tail
+  sample N + k it owns (k = t + i*TPS < cp, in order of i).
 """
 
 from __future__ import annotations
@@ -60,22 +65,36 @@ def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
     return [v.astype(np.uint32) for v in c]
 
 
-class Sfc32:
-    """SFC32 (Doty-Humphrey, PractRand): tmp = a + b + counter; a = b ^ (b >> 9);
-    b = c + (c << 3); c = rotl(c, 21) + tmp.  Vectorised over lanes; counter from 1."""
+MWC_A = np.uint64(4294883355)
+NOISE_PHASES = 64
+NOISE_MASK = np.uint32(0x1F8)
+SQRT_2LN2 = 1.1774100225154747
 
-    def __init__(self, a, b, c):
-        self.a, self.b, self.c = (np.asarray(v, np.uint32).copy() for v in (a, b, c))
-        self.n = np.uint32(0)
+
+class Mwc64x:
+    """MWC64X (D. B. Thomas): output x ^ c, then (c, x) <- hi / lo of A*x + c.  Vectorised
+    over lanes; seeded with x = P0, c = (P1 >> 1) | 1 (never a fixed point, c < A)."""
+
+    def __init__(self, p0, p1):
+        self.x = np.asarray(p0, np.uint64) & MASK32
+        self.c = ((np.asarray(p1, np.uint64) & MASK32) >> np.uint64(1)) | np.uint64(1)
 
     def next(self) -> np.ndarray:
-        with np.errstate(over="ignore"):
-            self.n = np.uint32(self.n + np.uint32(1))
-            r = self.a + self.b + self.n
-            self.a = self.b ^ (self.b >> np.uint32(9))
-            self.b = self.c + (self.c << np.uint32(3))
-            self.c = ((self.c << np.uint32(21)) | (self.c >> np.uint32(11))) + r
+        r = (self.x ^ self.c).astype(np.uint32)
+        v = MWC_A * self.x + self.c  # < 2^64: no wrap
+        self.x, self.c = v & MASK32, v >> np.uint64(32)
         return r
+
+
+class LaneStream:
+    """The lane block of every (symbol, lane): payload words and the continuing generator."""
+
+    def __init__(self, p0, p1, p2, p3):
+        self.gen = Mwc64x(p0, p1)
+        self.payload = np.stack([p2, p3, self.gen.next(), self.gen.next()], axis=1).astype(np.uint32)
+
+    def next(self) -> np.ndarray:
+        return self.gen.next()
 
 
 def geometry(N: int):
@@ -83,15 +102,33 @@ def geometry(N: int):
     return E, N // E
 
 
-def lane_generators(seed: int, s: np.ndarray, N: int) -> Sfc32:
-    """One SFC32 per (symbol, lane), lanes in row-major (s, t) order."""
+def lane_generators(seed: int, s: np.ndarray, N: int) -> LaneStream:
+    """One lane block per (symbol, lane), lanes in row-major (s, t) order."""
     E, tps = geometry(N)
     s = np.asarray(s, dtype=np.int64)
     ss = np.repeat(s, tps).astype(np.uint64)
     t = np.tile(np.arange(tps, dtype=np.uint64), len(s))
-    x, y, z, _ = philox4x32_10(t, ss & MASK32, ss >> np.uint64(32), np.full_like(t, K_LANE),
-                               seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    return Sfc32(x, y, z)
+    p = philox4x32_10(t, ss & MASK32, ss >> np.uint64(32), np.full_like(t, K_LANE),
+                      seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    return LaneStream(*p)
+
+
+def noise_table(sigma: float) -> np.ndarray:
+    """The 64 phase points times sigma sqrt(2 ln 2), float32 components (as built in LDS)."""
+    sc = np.float32(sigma * SQRT_2LN2)
+    th = np.pi * (2.0 * np.arange(NOISE_PHASES) + 1.0) / NOISE_PHASES
+    re = sc * np.cos(th).astype(np.float32)
+    im = sc * np.sin(th).astype(np.float32)
+    return re.astype(np.float64) + 1j * im.astype(np.float64)
+
+
+def noise_from_words(w: np.ndarray, sigma: float) -> np.ndarray:
+    """Complex normal of each 32-bit lane word (radius from the word with bits 3..8 set,
+    phase = bits 3..8 through the table)."""
+    w = np.asarray(w, np.uint32)
+    f = (w | NOISE_MASK).astype(np.float32)  # round to nearest even, as v_cvt_f32_u32
+    r = np.sqrt(32.0 - np.log2(f.astype(np.float64)))
+    return r * noise_table(sigma)[(w >> np.uint32(3)) & np.uint32(NOISE_PHASES - 1)]
 
 
 def _lane_to_row(v: np.ndarray, S: int, N: int) -> np.ndarray:
@@ -100,32 +137,21 @@ def _lane_to_row(v: np.ndarray, S: int, N: int) -> np.ndarray:
     return v.reshape(S, tps, E).transpose(0, 2, 1).reshape(S, N)
 
 
-def tx_indices(gen: Sfc32, S: int, N: int, b) -> np.ndarray:
-    """Constellation indices (S, N) from outputs 0..3 of every lane generator; b is the bits
-    per subcarrier, one value or one per subcarrier (adaptive loading)."""
+def tx_indices(gen: LaneStream, S: int, N: int, b) -> np.ndarray:
+    """Constellation indices (S, N) from the payload words of every lane; b is the bits per
+    subcarrier, one value or one per subcarrier (adaptive loading)."""
     E, _ = geometry(N)
-    words = np.stack([gen.next() for _ in range(4)], axis=1)  # (lanes, 4)
+    words = gen.payload  # (lanes, 4)
     i = np.arange(E)
     byte = (words[:, i >> 2] >> (8 * (i & 3)).astype(np.uint32)) & np.uint32(0xFF)
     mask = (np.int64(1) << np.broadcast_to(np.asarray(b, np.int64), (N,))) - 1
     return _lane_to_row(byte.astype(np.int64), S, N) & mask[None, :]
 
 
-def lane_noise(gen: Sfc32, S: int, N: int, sigma: float) -> np.ndarray:
-    """Complex noise (S, N) at the kept time samples, from outputs 4.. of every lane."""
+def lane_noise(gen: LaneStream, S: int, N: int, sigma: float) -> np.ndarray:
+    """Complex noise (S, N) at the kept time samples, from outputs m2 .. m(E+1) of every lane."""
     E, _ = geometry(N)
-    sig = np.float32(sigma)
-    m2s2ln2 = np.float32(-1.3862943611198906) * sig * sig  # -2 ln2 sigma^2 in float32
-    cols = []
-    for _ in range((E + 1) // 2):
-        u = [gen.next(), gen.next()]
-        a = gen.next()
-        v = [(a >> np.uint32(9)).astype(np.float64) * 2.0 ** -23, (a & np.uint32(0xFFFF)).astype(np.float64) * 2.0 ** -16]
-        for q in range(2):
-            uf = (u[q].astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -32)
-            r = np.sqrt(np.float64(m2s2ln2) * np.log2(uf.astype(np.float64)))
-            cols.append(r * np.exp(2j * np.pi * v[q]))
-    n = np.stack(cols[:E], axis=1)
+    n = np.stack([noise_from_words(gen.next(), sigma) for _ in range(E)], axis=1)
     return _lane_to_row(n, S, N)
 
 
@@ -147,8 +173,8 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
 
     modulator "OFDM" | "SC" (modulation/models.py:58-91), prefix "CP" | "ZP"
     (prefix/models.py:29-101), scheme "QAM" | "PSK".  With zero padding every lane draws,
-    after its elements' noise, one more noise triple per received tail sample
-    N + k (k = t + i*TPS < cp, in order of i) and uses its first sample.
+    after its elements' noise, one more noise word per received tail sample
+    N + k (k = t + i*TPS < cp, in order of i).
 
     orders: per-subcarrier QAM orders (CAPACITY_BASED bit loading, 0 = unused; M is then
     ignored).  As in the reference's decode (constellation/adaptive.py:259-263) a trailing
@@ -228,12 +254,6 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk)
 
 
-def lane_noise_tail(gen: Sfc32, sigma: float) -> np.ndarray:
-    """One noise triple per lane (all lanes draw; only lanes owning a tail sample use it)."""
-    sig = np.float32(sigma)
-    m2s2ln2 = np.float32(-1.3862943611198906) * sig * sig
-    u = [gen.next(), gen.next()]
-    a = gen.next()
-    uf = (u[0].astype(np.float32) + np.float32(0.5)) * np.float32(2.0 ** -32)
-    r = np.sqrt(np.float64(m2s2ln2) * np.log2(uf.astype(np.float64)))
-    return r * np.exp(2j * np.pi * (a >> np.uint32(9)).astype(np.float64) * 2.0 ** -23)
+def lane_noise_tail(gen: LaneStream, sigma: float) -> np.ndarray:
+    """One noise word per lane (all lanes draw; only lanes owning a tail sample use it)."""
+    return noise_from_words(gen.next(), sigma)

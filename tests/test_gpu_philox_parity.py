@@ -64,7 +64,7 @@ CASES = [
     (256, 0, "two_ray", "ZF", 1023, 30.0, B.OFDM_F32, {"adaptive": True}),   # up to 256-QAM
     (256, 0, "two_ray", "MMSE", 1024, 16.0, B.OFDM_F32, {"adaptive": True}),  # unused subcarriers
     (4096, 0, "Lin-Phoong_P1", "MMSE", 160, 26.0, B.OFDM_F32, {"adaptive": True}),
-    (64, 0, "default_multipath", "MMSE", 2049, 18.0, B.OFDM_F32, {"adaptive": True}),
+    (64, 0, "default_multipath", "MMSE", 4097, 18.0, B.OFDM_F32, {"adaptive": True}),
 ]
 
 

@@ -1,12 +1,13 @@
 """The throughput-mode stream definition restated in the oracle (oracle/philox_streams.py).
 
-CPU-only: Philox4x32-10 against the Random123 known-answer vectors, and the statistical
-and structural properties of the lane streams that the GPU parity tests
-(test_gpu_philox_parity.py) then hold the fused kernels to.
+CPU-only: Philox4x32-10 against the Random123 known-answer vectors, the MWC64X step against
+its defining recurrence, and the statistical and structural properties of the lane streams
+that the GPU parity tests (test_gpu_philox_parity.py) then hold the fused kernels to.
 """
 
 import numpy as np
 import pytest
+from scipy.stats import norm
 
 import philox_streams as P
 
@@ -23,19 +24,40 @@ def test_philox4x32_10_known_answers(ctr, key, want):
     assert tuple(int(g[0]) for g in got) == want
 
 
-def test_sfc32_counter_starts_at_one():
-    g = P.Sfc32([1], [2], [3])
-    assert int(g.next()[0]) == 1 + 2 + 1
-    assert int(g.a[0]) == 2 ^ (2 >> 9) and int(g.b[0]) == 3 + (3 << 3)
+def test_mwc64x_recurrence():
+    """MWC64X: output x ^ c, then A*x + c split into (carry, x); seeded c = (P1 >> 1) | 1."""
+    p0, p1 = 0x89ABCDEF, 0xFFFFFFFF
+    g = P.Mwc64x([p0], [p1])
+    x, c = p0, (p1 >> 1) | 1
+    for _ in range(50):
+        assert int(g.next()[0]) == x ^ c
+        v = 4294883355 * x + c
+        x, c = v & 0xFFFFFFFF, v >> 32
+        assert c < 4294883355
+
+
+def test_lane_payload_words():
+    """payload = (P2, P3, m0, m1) of the lane's Philox block and generator."""
+    seed, s, N = 0x1234_5678_9ABC, np.array([3, 2**33 + 5]), 256
+    lanes = P.lane_generators(seed, s, N)
+    tps = N // 16
+    lane = tps + 7  # symbol 2**33 + 5, lane 7
+    p = P.philox4x32_10(np.array([7], np.uint64), np.array([5], np.uint64), np.array([2], np.uint64),
+                        np.array([P.K_LANE], np.uint64), seed & 0xFFFFFFFF, seed >> 32)
+    g = P.Mwc64x(p[0], p[1])
+    want = [int(p[2][0]), int(p[3][0]), int(g.next()[0]), int(g.next()[0])]
+    assert [int(w) for w in lanes.payload[lane]] == want
+    assert int(lanes.next()[lane]) == int(g.next()[0])
 
 
 def test_lane_streams_depend_only_on_seed_and_symbol():
     a = P.lane_generators(7, np.arange(10, 20), 1024)
     b = P.lane_generators(7, np.arange(15, 20), 1024)
+    assert np.array_equal(a.payload[5 * 64:], b.payload)
     wa, wb = a.next(), b.next()
     assert np.array_equal(wa[5 * 64:], wb)
     c = P.lane_generators(8, np.arange(10, 20), 1024)
-    assert not np.array_equal(c.next(), wa)
+    assert not np.array_equal(c.payload, a.payload)
 
 
 @pytest.mark.parametrize("N,b", [(1024, 6), (64, 2), (16, 4), (4096, 8)])
@@ -48,20 +70,45 @@ def test_payload_bits_uniform(N, b):
     assert np.all(np.abs(counts - exp) < 6 * np.sqrt(exp))
 
 
+@pytest.mark.parametrize("phi", [0.0, np.pi / 7, np.pi / 4, 0.3])
+def test_phase_table_projection_tails(phi):
+    """Noise = Rayleigh radius x one of 64 phase points: the projection on any direction phi has
+    the Gaussian tail P(> d sigma) = (1/64) sum_j exp(-d^2 / (2 cos^2(theta_j - phi))) to the
+    trapezoid rule's accuracy on that smooth periodic integrand."""
+    th = 2 * np.pi * (np.arange(P.NOISE_PHASES) + 0.5) / P.NOISE_PHASES - phi
+    c = np.cos(th)
+    c = c[c > 0]
+    for d, tol in ((1.0, 3e-6), (2.0, 1e-8), (3.0, 1e-9), (3.7, 1e-10), (4.5, 1e-10)):
+        p = np.exp(-d * d / (2 * c * c)).sum() / P.NOISE_PHASES
+        assert abs(p / norm.sf(d) - 1) < tol, (d, p, norm.sf(d))
+
+
+def test_radius_words():
+    """radius^2 sigma^2 2 ln2 (32 - log2(w | 0x1F8)) = -2 sigma^2 ln u, u = (w | 0x1F8) 2^-32;
+    truncated at u = 504 2^-32 (5.65 sigma), never zero."""
+    w = np.array([0, 0x1F8, 0xFFFFFFFF, 1 << 20], np.uint32)
+    n = P.noise_from_words(w, 1.0)
+    u = (w | 0x1F8).astype(np.float64) / 2.0 ** 32
+    u[2] = 1.0  # float32(0xFFFFFFFF) rounds to 2^32
+    assert np.allclose(np.abs(n), np.sqrt(-2 * np.log(u)), rtol=1e-6)
+    assert abs(np.abs(n[0]) - 5.6498) < 1e-3
+
+
 def test_noise_is_complex_gaussian():
     S, N, sigma = 400, 1024, 0.3
     g = P.lane_generators(5, np.arange(S), N)
-    P.tx_indices(g, S, N, 6)
     n = P.lane_noise(g, S, N, sigma).ravel()
-    for comp in (n.real, n.imag):
+    for comp in (n.real, n.imag, (n * np.exp(-0.4j)).real):
         assert abs(comp.mean()) < 5 * sigma / np.sqrt(n.size)
         assert abs(comp.var() / sigma ** 2 - 1) < 0.01
         k = np.mean((comp / sigma) ** 4)
         assert abs(k - 3) < 0.05
-    # tails: P(|n_re| > 3 sigma) = 2.7e-3
-    tail = np.mean(np.abs(n.real) > 3 * sigma)
-    assert abs(tail / 2.6998e-3 - 1) < 0.05
+        # tails: P(|n| > 3 sigma) = 2.7e-3, P(|n| > 4 sigma) = 6.3e-5
+        assert abs(np.mean(np.abs(comp) > 3 * sigma) / 2.6998e-3 - 1) < 0.05
+        assert abs(np.mean(np.abs(comp) > 4 * sigma) / 6.334e-5 - 1) < 0.25
     assert abs(np.corrcoef(n.real, n.imag)[0, 1]) < 0.01
+    # neighbouring time samples are uncorrelated
+    assert abs(np.corrcoef(n.real[:-1], n.real[1:])[0, 1]) < 0.01
 
 
 def test_oracle_link_noise_free_is_error_free():
