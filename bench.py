@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1500, help="OFDM symbols per CPU worker")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ber-check", action="store_true", help="skip the BER Delta-dB check vs the reference streams")
+    ap.add_argument("--ramp-seconds", type=float, default=0.25,
+                    help="untimed warmup beyond --warmup until this much GPU time has passed (clock ramp)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -180,6 +182,22 @@ def main():
 
     for i in range(args.warmup):
         engine.run(total, snr, seed=10_000 + i, group=group)
+    torch.cuda.synchronize()
+    # Clock ramp: a fresh box idles at ~100-350 MHz and its clock needs ~40 ms of load to reach
+    # the steady state the power cap sets (tools/ramp_probe.py, profiles/r02_ramp_b.json), longer
+    # than a few warmup steps.  Keep warming up (untimed, outside the K timed steps) until
+    # --ramp-seconds of GPU work have run; the extra steps are reported.
+    ramp_steps, t_ramp = 0, time.perf_counter()
+    while args.ramp_seconds > 0:
+        done = torch.tensor([time.perf_counter() - t_ramp >= args.ramp_seconds], dtype=torch.int32, device="cuda")
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(done, op=dist.ReduceOp.MIN)  # every rank runs the same number of steps
+        if int(done.item()):
+            break
+        engine.run(total, snr, seed=20_000 + ramp_steps, group=group)
+        ramp_steps += 1
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -220,6 +238,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "clock_ramp": {"extra_untimed_steps": ramp_steps, "seconds": args.ramp_seconds},
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",

@@ -51,7 +51,36 @@
 #define OFDM_RX_FAST_BLOCK 512
 #endif
 
+// Streaming (nontemporal) loads of the channel samples in RX: y is read exactly once, and
+// the nontemporal hint lifts the achievable read rate of this access pattern on MI355X from
+// 6.2 to 7.1 TB/s (tools/hbm_probe.hip).  TX stores: the same hint, off by default (no gain
+// measured on the write side).
+#ifndef OFDM_RX_NT
+#define OFDM_RX_NT 1
+#endif
+#ifndef OFDM_TX_NT
+#define OFDM_TX_NT 0
+#endif
+
 namespace ofdm {
+
+template <bool NT, typename C>
+__device__ __forceinline__ C ld_stream(const C* p) {
+    if constexpr (NT && sizeof(C) == 8) {
+        C v;
+        v.v = __builtin_nontemporal_load((const f32x2*)p);
+        return v;
+    } else {
+        return *p;
+    }
+}
+template <bool NT, typename C>
+__device__ __forceinline__ void st_stream(C* p, C v) {
+    if constexpr (NT && sizeof(C) == 8)
+        __builtin_nontemporal_store(v.v, (f32x2*)p);
+    else
+        *p = v;
+}
 
 // MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
 #ifndef OFDM_TX_MP_BLOCK
@@ -65,8 +94,30 @@ constexpr int tx_block() {
 }
 // padded FIR row index of the throughput multipath TX: one slot per 16 elements
 __host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
+// Throughput RX (FB > 1, N <= 1024) software-pipelines its HBM loads: while a wave works on
+// one symbol, the channel samples of its next symbol are already in flight into registers
+// (E more VGPR pairs), so the load latency overlaps the FFT / noise / slicer instead of
+// waiting on a wave switch.  256-thread workgroups at OFDM_RX_PF_WAVES waves per SIMD.
+// Off: measured slower on MI355X (config b RX 1.90 -> 2.16 ms, c 2.72 -> 3.52 ms per 1e6
+// symbols at 3 waves/SIMD) -- the chip runs at its 1400 W power cap, so the overlap buys no
+// issue slots and the lower occupancy costs latency hiding in the FFT's LDS transposes.
+#ifndef OFDM_RX_PREFETCH
+#define OFDM_RX_PREFETCH 0
+#endif
+#ifndef OFDM_RX_PF_WAVES
+#define OFDM_RX_PF_WAVES 3
+#endif
+template <int FB, int LOGN>
+constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && FB > 1 && LOGN >= 6 && LOGN <= 10; }
 template <int FB, int LOGN, int EQ>
-constexpr int rx_block() { return FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock; }
+constexpr int rx_block() {
+    return rx_prefetch<FB, LOGN>() ? kBlock
+                                    : (FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock);
+}
+template <int FB, int LOGN, int EQ>
+constexpr int rx_waves() {
+    return rx_prefetch<FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
+}
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 
 // Reference mode: stage OFDM symbol s's tx bits from the packed bytes of the run
@@ -385,7 +436,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
 #pragma unroll
                     for (int i = 0; i < E; ++i) {
                         const C yv = FOLD_H0 ? x[i] : cmul(h0, x[i]);
-                        if (yout && !(a.flags & 4)) yo[t + i * TPS] = yv;
+                        if (yout && !(a.flags & 4)) st_stream<(FB > 0 && OFDM_TX_NT)>(yo + t + i * TPS, yv);
                     }
                     if (zp && yout)
                         for (int j = t; j < cp; j += TPS) yo[N + j] = mk<R>(0, 0);
@@ -535,7 +586,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
 // ============================================================ fused RX
 // EQ: OFDM_EQ_* fixed at compile time (throughput kernel) or -1 = from the plan.
 template <typename R, int LOGN, int EQ, int FB>
-__global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<FB, LOGN, EQ>(), OFDM_RX_WAVES))) void k_rx(
+__global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>())) void k_rx(
     RxArgs a) {
     constexpr int BLK = rx_block<FB, LOGN, EQ>();
     using G = Geo<LOGN, BLK>;
@@ -631,22 +682,36 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (block_waves(rx_block<F
     const int64_t niter = (cm.n_sym + G::SPB - 1) / G::SPB;
     unsigned long long be = 0, se = 0;
 
+    // kept channel samples of local symbol sl (zeros past the end / when ablated)
+    auto load_sym = [&](int64_t sl, C (&dst)[E]) {
+        const C* ys = (const C*)a.y + sl * ystride;
+        if (sl < cm.n_sym && !(a.flags & 16)) {
+#pragma unroll
+            for (int i = 0; i < E; ++i) dst[i] = ld_stream<(FB > 0 && OFDM_RX_NT)>(ys + t + i * TPS);
+        } else {
+#pragma unroll
+            for (int i = 0; i < E; ++i) dst[i] = mk<R>(0, 0);
+        }
+    };
+    constexpr bool PF = rx_prefetch<FB, LOGN>();
+    C xn[PF ? E : 1];  // prefetched samples of the wave's next symbol
+    if constexpr (PF) load_sym((int64_t)blockIdx.x * G::SPB + ls, xn);
+
     for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
         const int64_t sl = it * G::SPB + ls;
         const int64_t sg = cm.sym0 + sl;
         const bool active = sl < cm.n_sym;
         TxBits<FB, TPS> tb;
-        if (!OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
         // kept channel samples + AWGN; the 1/sqrt(N) of fft(norm="ortho") folded in
         const C* ys = (const C*)a.y + sl * ystride;
         C x[E];
-        if (active && !(a.flags & 16)) {
+        if constexpr (PF) {
 #pragma unroll
-            for (int i = 0; i < E; ++i) x[i] = ys[t + i * TPS];
-        } else {
-#pragma unroll
-            for (int i = 0; i < E; ++i) x[i] = mk<R>(0, 0);
+            for (int i = 0; i < E; ++i) x[i] = xn[i];
+            load_sym(sl + (int64_t)gridDim.x * G::SPB, xn);  // in flight during this symbol
         }
+        if (!OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
+        if constexpr (!PF) load_sym(sl, x);
         if (OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
         if (OFDM_RX_NOISE_FIRST == 1 && sizeof(R) == 4 && active && noise && !array_noise) {
             // the lane's noise while the loads are in flight, then one add per element

@@ -9,8 +9,16 @@
 
 namespace ofdm {
 
+// OFDM_AB_ONLY: experiment builds (Makefile VARIANT=..., tools/ab.sh) instantiate only the
+// N = 1024, 64-QAM kernels of bench configs (b) and (c) -- a minute's compile instead of several
+#ifdef OFDM_AB_ONLY
+#define OFDM_LOGN_CASES(X) X(10)
+#define OFDM_FB_CASES(X) X(6)
+#else
 #define OFDM_LOGN_CASES(X) \
     X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+#define OFDM_FB_CASES(X) X(2) X(4) X(6) X(8)
+#endif
 
 template <typename F>
 static hipError_t set_smem(F fn, size_t bytes) {
@@ -26,6 +34,27 @@ constexpr int kFastMinLogN = 6;  // throughput specialisations for N >= 64
 
 static inline int clamp_grid(int64_t want) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, kMaxGrid));
+}
+
+// Persistent grid for a grid-stride kernel: as many workgroups as the device holds at once
+// (occupancy x CUs, queried once per kernel and device), so no partial last round of
+// workgroups idles part of the chip.
+template <typename F>
+static int resident_grid(F fn, int blk, size_t smem) {
+    static int cached[16] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+    if (cached[dev] == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), blk, smem) !=
+                hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return kMaxGrid;
+        }
+        cached[dev] = std::max(1, std::min(kMaxGrid, per_cu * cus));
+    }
+    return cached[dev];
 }
 
 template <typename R, int LOGN, int MODE>
@@ -145,13 +174,14 @@ static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
             return tx_fast<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && (!a.c.nn || a.c.psk_m > 0)) {  // OFDM / SC, CP / ZP, QAM / PSK
+#define OFDM_TX_FB(F) \
+    case F:              \
+        return tx_fast<R, LOGN, F>(a, grid, s);
             switch (a.c.b) {
-                case 2: return tx_fast<R, LOGN, 2>(a, grid, s);
-                case 4: return tx_fast<R, LOGN, 4>(a, grid, s);
-                case 6: return tx_fast<R, LOGN, 6>(a, grid, s);
-                case 8: return tx_fast<R, LOGN, 8>(a, grid, s);
+                OFDM_FB_CASES(OFDM_TX_FB)
                 default: break;
             }
+#undef OFDM_TX_FB
         }
     }
     return tx_launch<R, LOGN, 0, -1>(a, grid, s);
@@ -179,6 +209,7 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
+    if constexpr (rx_prefetch<FB, LOGN>()) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
@@ -201,13 +232,14 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
             return rx_eq<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
             (!a.c.nn || a.c.psk_m > 0)) {  // OFDM / SC, CP / ZP, QAM / PSK
+#define OFDM_RX_FB(F) \
+    case F:              \
+        return rx_eq<R, LOGN, F>(a, grid, s);
             switch (a.c.b) {
-                case 2: return rx_eq<R, LOGN, 2>(a, grid, s);
-                case 4: return rx_eq<R, LOGN, 4>(a, grid, s);
-                case 6: return rx_eq<R, LOGN, 6>(a, grid, s);
-                case 8: return rx_eq<R, LOGN, 8>(a, grid, s);
+                OFDM_FB_CASES(OFDM_RX_FB)
                 default: break;
             }
+#undef OFDM_RX_FB
         }
     }
     return rx_launch<R, LOGN, -1, 0>(a, grid, s);
