@@ -57,6 +57,12 @@ CASES = [
     (128, 4, "severe_multipath", "MMSE", 1024, 8.0, B.OFDM_F32, {"scheme": "PSK"}),
     (1024, 16, "severe_multipath", "MMSE", 128, 16.0, B.OFDM_F32, {"scheme": "PSK"}),
     (512, 32, "Lin-Phoong_P1", "ZF", 128, 22.0, B.OFDM_F32, {"scheme": "PSK"}),
+    # 4- and 16-PSK take the throughput kernels (FB = 2 / 4) with sector decisions: with
+    # SC-OFDM's unscaled IFFT, with the zero-padding overlap-add and its tail noise, and both
+    (256, 16, "Lin-Phoong_P1", "MMSE", 256, 20.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC", "prefix": "ZP"}),
+    (128, 4, "severe_multipath", "ZF", 1024, 10.0, B.OFDM_F32, {"scheme": "PSK", "prefix": "ZP"}),
+    (256, 16, "two_ray", "MMSE", 256, 18.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC"}),
+    (512, 4, "Lin-Phoong_P1", "MMSE", 256, 9.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC"}),
     # CAPACITY_BASED bit loading (config d): per-subcarrier orders from water-filling at the SNR;
     # an odd symbol count leaves a trailing partial byte that is not compared
     (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F32, {"adaptive": True}),

@@ -75,6 +75,25 @@ __global__ __launch_bounds__(512) void k_write_sym(f2* __restrict__ a, size_t ns
     }
 }
 
+// the same symbols with 16-byte lanes: lane t writes elements 2t, 2t+1 + 128 i (8 x 1 KB per wave)
+template <bool NT>
+__global__ __launch_bounds__(512) void k_write_sym4(f4* __restrict__ a, size_t nsym, float v) {
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    for (size_t s = blockIdx.x * 8ull + w; s < nsym; s += (size_t)gridDim.x * 8) {
+        f4* p = a + s * 512 + t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st<f4, NT>(p + 64 * i, f4{v, (float)i, v, v});
+    }
+}
+// one-shot grid (no grid-stride loop): workgroup g writes its own 64 KB chunk, 4 x 16 B per
+// thread at a 8 KB stride (the launch-order moving window an elementwise kernel produces)
+__global__ __launch_bounds__(512) void k_write_chunk(f4* __restrict__ a, size_t n, float v) {
+    const size_t base = (size_t)blockIdx.x * 2048 + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (base + 512 * i < n) a[base + 512 * i] = f4{v, v, v, (float)i};
+}
+
 __global__ __launch_bounds__(512) void k_copy(const f4* __restrict__ a, f4* __restrict__ b, size_t n) {
     for (size_t i = blockIdx.x * 512ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 512) b[i] = a[i];
 }
@@ -136,9 +155,13 @@ int main() {
         printf(", \"write_x4_nt\": %.0f", B / timed([&] { k_write4<true><<<grid, 512>>>(b, n, 1.f); }, 5));
         printf(", \"write_sym\": %.0f", B / timed([&] { k_write_sym<false><<<grid, 512>>>((f2*)b, nsym, 1.f); }, 5));
         printf(", \"write_sym_nt\": %.0f", B / timed([&] { k_write_sym<true><<<grid, 512>>>((f2*)b, nsym, 1.f); }, 5));
+        printf(", \"write_sym4\": %.0f", B / timed([&] { k_write_sym4<false><<<grid, 512>>>(b, nsym, 1.f); }, 5));
+        printf(", \"write_sym4_nt\": %.0f", B / timed([&] { k_write_sym4<true><<<grid, 512>>>(b, nsym, 1.f); }, 5));
         printf(", \"copy\": %.0f", 2 * B / timed([&] { k_copy<<<grid, 512>>>(a, b, n); }, 5));
         printf(", \"read+write_nt\": %.0f}", 2 * B / timed([&] { k_mix<<<2 * grid, 512>>>(a, b, n, out); }, 5));
     }
+    printf(", \"write_chunk_oneshot\": %.0f",
+           (double)bytes / 1e6 / timed([&] { k_write_chunk<<<(unsigned)((n + 2047) / 2048), 512>>>(b, n, 2.f); }, 5));
     CHECK(hipGetLastError());
     printf("}\n");
     return 0;
