@@ -36,17 +36,49 @@ CONFIGS = {
           "config (b): N_FFT=1024, 64-QAM, flat channel (flat_fading.npy, cp=0), no equaliser, AWGN 24 dB"),
     "c": (1024, 64, "severe_multipath", 1.0, "MMSE", 27.75,
           "config (c): N_FFT=1024, 64-QAM, severe_multipath.npy (8 taps, cp=7), MMSE, AWGN 27.75 dB"),
+    # M = 0: CAPACITY_BASED adaptive bit loading (per-subcarrier square-QAM orders from the
+    # water-filling allocation at the SNR, simulation/models.py:289-395)
+    "d": (2048, 0, "Lin-Phoong_P1", 1.0, "MMSE", 20.0,
+          "config (d): N_FFT=2048, adaptive bit loading (water-filling, desired SER 1e-3), Lin-Phoong_P1.npy "
+          "(4 taps, cp=3), MMSE, AWGN 20 dB"),
     "e": (4096, 256, "Lin-Phoong_P1", 1.0, "MMSE", 30.0,
           "config (e): N_FFT=4096, 256-QAM, Lin-Phoong_P1.npy (4 taps, cp=3), MMSE, AWGN 30 dB"),
 }
+
+
+def make_engine(cfg, precision):
+    """LinkEngine of a bench config; the constellation tables as Simulation builds them
+    (QAMConstellationMapper, or the adaptive mapper over the water-filling orders)."""
+    from ofdm_based_systems import _backend as B
+    from ofdm_based_systems.constellation.adaptive import AdaptiveConstellationMapper
+    from ofdm_based_systems.constellation.models import QAMConstellationMapper
+    from ofdm_based_systems.engine import LinkEngine
+    from ofdm_based_systems.power_allocation.models import WaterfillingPowerAllocation
+
+    N, M, ch, ratio, eq_name, snr, _ = cfg
+    h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+    cp = int(ratio * (len(h) - 1))
+    eq = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}[eq_name]
+    sc = None
+    if M == 0:
+        gains = np.abs(np.fft.fft(h, N)) ** 2
+        noise_power = 10 ** (-snr / 10)
+        alloc = WaterfillingPowerAllocation(N, gains, noise_power).allocate()
+        orders = np.array([QAMConstellationMapper.calculate_bit_loading_order(ser=1e-3, snr=p * g / noise_power)
+                           for p, g in zip(alloc, gains)], dtype=np.int64)
+        luts, sc = AdaptiveConstellationMapper(orders, QAMConstellationMapper, N).lut_tables()
+    else:
+        luts = [QAMConstellationMapper(M).constellation]
+    return LinkEngine(N, cp, h, eq, luts, sc, precision), h, cp
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def kernel_bytes_per_symbol(N: int, b: int, cp: int) -> int:
+def kernel_bytes_per_symbol(N: int, bps: int, cp: int) -> int:
     """Algorithmic bytes one OFDM symbol moves in ONE of the two kernels:
-    B_alg = 2*ceil(N*b/8) + 2*(N+cp)*8 per symbol is split evenly: each kernel touches the tx
-    bits once (map / comparator) and the complex64 channel stream once (write / read)."""
-    return math.ceil(N * b / 8) + (N + cp) * 8
+    B_alg = 2*ceil(bps/8) + 2*(N+cp)*8 per symbol (bps = N*b, or sum b_k with adaptive loading)
+    is split evenly: each kernel touches the tx bits once (map / comparator) and the complex64
+    channel stream once (write / read)."""
+    return math.ceil(bps / 8) + (N + cp) * 8
 
 
 def _cpu_worker(args):
@@ -55,6 +87,13 @@ def _cpu_worker(args):
 
     seed, S, N, M, ch, cp, eq, snr = args
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+    if M == 0:  # CAPACITY_BASED: orders from water-filling, the adaptive data path
+        orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
+        bps = int(sum(int(np.log2(o)) for o in orders if o > 0))
+        tx, nz = O.reference_streams(seed, S * bps, S * (N + cp))
+        t0 = time.perf_counter()
+        O.run_adaptive(tx, orders, N, h, cp, eq, snr, nz)
+        return S, time.perf_counter() - t0
     b = int(np.log2(M))
     tx, nz = O.reference_streams(seed, S * N * b, S * (N + cp))
     t0 = time.perf_counter()
@@ -88,7 +127,7 @@ def cpu_baseline(cfg, per_worker: int):
     }
 
 
-def ber_vs_reference(engine64, N, M, cp, snr, ber_phx, bits_phx, symbols=16000, seed=1):
+def ber_vs_reference(engine64, N, cp, snr, ber_phx, bits_phx, symbols=16000, seed=1):
     """BER Delta dB of the timed throughput run against the reference-stream path at the same SNR.
 
     The reference-stream path is the drop-in's default mode: the reference's own PCG64 bytes and
@@ -97,15 +136,13 @@ def ber_vs_reference(engine64, N, M, cp, snr, ber_phx, bits_phx, symbols=16000, 
     horizontal distance between the two BER curves at the throughput run's BER, through the
     reference curve's local slope from a second point 0.5 dB higher; positive = the throughput
     run needs more SNR.  Outside the timed region."""
-    b = int(np.log2(M))
-
     def ref_ber(snr_db, sd):
-        bits = np.random.Generator(np.random.PCG64(sd)).bytes(symbols * N * b // 8)
+        bits = np.random.Generator(np.random.PCG64(sd)).bytes(math.ceil(symbols * engine64.bps / 8))
         rs = np.random.RandomState(sd)  # = np.random.seed(sd) + np.random.normal (the reference's draws)
         nr = rs.normal(size=symbols * (N + cp))
         ni = rs.normal(size=symbols * (N + cp))
         r = engine64.run(symbols, snr_db, bits=np.frombuffer(bits, np.uint8), normals=(nr, ni))
-        return r.bit_errors, symbols * N * b
+        return r.bit_errors, engine64.valid_bits(symbols)
 
     e0, n0 = ref_ber(snr, seed)
     e1, n1 = ref_ber(snr + 0.5, seed + 1)
@@ -138,12 +175,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--symbols", type=int, default=1_000_000, help="OFDM symbols per GPU per step")
+    ap.add_argument("--symbols", type=int, default=0,
+                    help="OFDM symbols per GPU per step (default 1e6 x 1024/N: 8.2 GB of channel samples)")
     ap.add_argument("--config", default="b", choices=sorted(CONFIGS))
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
-    ap.add_argument("--cpu-sample", type=int, default=1500, help="OFDM symbols per CPU worker")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="OFDM symbols per CPU worker (default 1500 x 1024/N)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ber-check", action="store_true", help="skip the BER Delta-dB check vs the reference streams")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--ramp-seconds", type=float, default=0.25,
                     help="untimed warmup beyond --warmup until this much GPU time has passed (clock ramp)")
     args = ap.parse_args()
@@ -151,27 +191,28 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # OFDM_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a 1-GPU box
+    # (with --backend gloo; RCCL refuses two ranks on one GPU)
+    dev = int(os.environ.get("OFDM_BENCH_DEVICE", local))
+    torch.cuda.set_device(dev)
     group = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.backend)
         group = dist.group.WORLD
 
     from ofdm_based_systems import _backend as B
-    from ofdm_based_systems.constellation.models import QAMConstellationMapper
-    from ofdm_based_systems.engine import LinkEngine
 
     cfg = CONFIGS[args.config]
     N, M, ch, ratio, eq_name, snr, desc = cfg
-    h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
-    cp = int(ratio * (len(h) - 1))
-    b = int(np.log2(M))
-    eq = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}[eq_name]
     prec = B.OFDM_F32 if args.precision == "f32" else B.OFDM_F64
-    engine = LinkEngine(N, cp, h, eq, [QAMConstellationMapper(M).constellation], None, prec)
-    per_gpu = args.symbols
+    engine, h, cp = make_engine(cfg, prec)
+    bps = engine.bps  # bits per OFDM symbol
+    per_gpu = args.symbols if args.symbols else 1_000_000 // max(1, N // 1024)
     total = per_gpu * world
 
     def barrier():
@@ -227,7 +268,7 @@ def main():
     avg = {k: sum(d for d, _ in v) / len(v) for k, v in durs.items()}
     dom = max(avg, key=avg.get)
     sym_per_launch = durs[dom][0][1]
-    alg = kernel_bytes_per_symbol(N, b, cp) * sym_per_launch
+    alg = kernel_bytes_per_symbol(N, bps, cp) * sym_per_launch
     achieved = alg / avg[dom] / 1e9
     traffic = pmc_traffic(args.config, sym_per_launch)
     value = total * args.steps / elapsed
@@ -248,7 +289,8 @@ def main():
                 "on the GPU per (seed, symbol)",
         "config": {
             "workload": f"{desc}; {per_gpu} OFDM symbols per GPU per step",
-            "n_fft": N, "qam_order": M, "cp": cp, "channel": ch, "equalizer": eq_name, "snr_db": snr,
+            "n_fft": N, "qam_order": M if M else "adaptive", "bits_per_ofdm_symbol": bps, "cp": cp,
+            "channel": ch, "equalizer": eq_name, "snr_db": snr,
             "symbols_per_step": total, "parallelism": f"symbol-sharded x{world}",
         },
         "roofline": {
@@ -259,19 +301,20 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": None if traffic is None else traffic.get(dom),
-            "alg_bytes_per_symbol": kernel_bytes_per_symbol(N, b, cp),
+            "alg_bytes_per_symbol": kernel_bytes_per_symbol(N, bps, cp),
             "symbols_per_launch": sym_per_launch,
             "avg_launch_ms": {k: v * 1e3 for k, v in avg.items()},
         },
-        "path_hbm_fraction": value * 2 * kernel_bytes_per_symbol(N, b, cp) / (HBM_PEAK_GBS * 1e9 * world),
-        "ber": bit_errors / (total * args.steps * N * b),
+        "path_hbm_fraction": value * 2 * kernel_bytes_per_symbol(N, bps, cp) / (HBM_PEAK_GBS * 1e9 * world),
+        "ber": bit_errors / (engine.valid_bits(total) * args.steps),
     }
     if rank == 0 and not args.no_ber_check:
-        eng64 = LinkEngine(N, cp, h, eq, [QAMConstellationMapper(M).constellation], None, B.OFDM_F64)
-        out["ber_vs_reference"] = ber_vs_reference(eng64, N, M, cp, snr, out["ber"],
-                                                   total * args.steps * N * b)
+        eng64, _, _ = make_engine(cfg, B.OFDM_F64)
+        out["ber_vs_reference"] = ber_vs_reference(eng64, N, cp, snr, out["ber"],
+                                                   engine.valid_bits(total) * args.steps,
+                                                   symbols=max(2000, 16000 * 1024 // N))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample)
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or max(100, 1500 * 1024 // N))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -81,6 +81,34 @@ __device__ __forceinline__ void st_stream(C* p, C v) {
     else
         *p = v;
 }
+template <bool NT>
+__device__ __forceinline__ void st_stream(__attribute__((address_space(1))) cpx<float>* p, cpx<float> v) {
+    typedef __attribute__((address_space(1))) f32x2 gf2;
+    if constexpr (NT)
+        __builtin_nontemporal_store(v.v, (gf2*)p);
+    else
+        *(gf2*)p = v.v;
+}
+
+// Global-memory (address space 1) pointers: a pointer rebuilt from an integer would
+// otherwise be generic and compile to flat_* instructions.
+template <typename T>
+using gptr = __attribute__((address_space(1))) T*;
+
+// A wave-uniform pointer held in SGPRs (readfirstlane of both halves).
+template <typename T>
+__device__ __forceinline__ gptr<T> uniform_ptr(T* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (gptr<T>)(((uint64_t)hi << 32) | lo);
+}
+// base + element offset as (64-bit base) + zext(32-bit byte offset): the addressing the
+// global_load/store SGPR-base form matches
+template <typename T>
+__device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
+    return (gptr<T>)((__attribute__((address_space(1))) char*)base + (uint64_t)(elem * (uint32_t)sizeof(T)));
+}
 
 // MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
 #ifndef OFDM_TX_MP_BLOCK
@@ -436,7 +464,16 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
 #pragma unroll
                     for (int i = 0; i < E; ++i) {
                         const C yv = FOLD_H0 ? x[i] : cmul(h0, x[i]);
-                        if (yout && !(a.flags & 4)) st_stream<(FB > 0 && OFDM_TX_NT)>(yo + t + i * TPS, yv);
+                        if (!yout || (a.flags & 4)) continue;
+                        if constexpr (FB > 0 && TPS >= 64) {
+                            // the row base is wave-uniform: made explicit, the stores take the
+                            // SGPR-base + 32-bit lane-offset form instead of a loop-carried 64-bit
+                            // VGPR pointer (which spilled to scratch, and whose per-symbol reload's
+                            // vmcnt(0) waited for all of the previous symbol's stores)
+                            st_stream<OFDM_TX_NT>(lane_ptr(uniform_ptr(yo), (uint32_t)(t + i * TPS)), yv);
+                        } else {
+                            st_stream<(FB > 0 && OFDM_TX_NT)>(yo + t + i * TPS, yv);
+                        }
                     }
                     if (zp && yout)
                         for (int j = t; j < cp; j += TPS) yo[N + j] = mk<R>(0, 0);

@@ -36,6 +36,9 @@ static inline int clamp_grid(int64_t want) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, kMaxGrid));
 }
 
+#ifndef OFDM_PERSISTENT
+#define OFDM_PERSISTENT 0
+#endif
 // Persistent grid for a grid-stride kernel: as many workgroups as the device holds at once
 // (occupancy x CUs, queried once per kernel and device), so no partial last round of
 // workgroups idles part of the chip.
@@ -146,6 +149,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     if (e != hipSuccess) return e;
     const int64_t groups = (a.c.n_sym + a.chunk - 1) / a.chunk;
     *grid = clamp_grid((groups + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
+    if (OFDM_PERSISTENT && FB > 0) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
@@ -209,7 +213,7 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
-    if constexpr (rx_prefetch<FB, LOGN>()) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
+    if (rx_prefetch<FB, LOGN>() || (OFDM_PERSISTENT && FB > 0)) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }

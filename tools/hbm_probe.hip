@@ -12,6 +12,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #define CHECK(x)                                                                      \
     do {                                                                              \
@@ -130,7 +131,40 @@ static float timed(F f, int reps) {
     return ms / reps;
 }
 
-int main() {
+// tools/hbm_probe loop <MiB> <seconds>: write-then-read batches of <MiB> back to back for
+// <seconds> (package power / clock sampled outside, tools/ic_power.sh)
+static int loop_mode(size_t mb, double seconds) {
+    const size_t ns = mb * (1u << 20) / 8192;
+    f2* b;
+    float* out;
+    CHECK(hipMalloc(&b, ns * 8192));
+    CHECK(hipMalloc(&out, 1 << 20));
+    int cus = 0;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int per_batch = (int)(2048 / mb) + 1;
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    double total_ms = 0, bytes = 0;
+    while (total_ms < seconds * 1e3) {
+        CHECK(hipEventRecord(e0, 0));
+        for (int r = 0; r < per_batch; ++r) {
+            k_write_sym<false><<<cus * 2, 512>>>(b, ns, 1.f);
+            k_read_sym<true><<<cus * 2, 512>>>(b, ns, out);
+        }
+        CHECK(hipEventRecord(e1, 0));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        total_ms += ms;
+        bytes += 2.0 * per_batch * ns * 8192;
+    }
+    printf("{\"batch_MiB\": %zu, \"seconds\": %.2f, \"write+read_GBps\": %.0f}\n", mb, total_ms / 1e3, bytes / total_ms / 1e6);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc >= 4 && std::string(argv[1]) == "loop") return loop_mode(std::stoul(argv[2]), std::stod(argv[3]));
     const size_t nsym = 1000000;
     const size_t bytes = nsym * 1024 * 8;
     const size_t n = bytes / 16;
@@ -160,6 +194,23 @@ int main() {
         printf(", \"copy\": %.0f", 2 * B / timed([&] { k_copy<<<grid, 512>>>(a, b, n); }, 5));
         printf(", \"read+write_nt\": %.0f}", 2 * B / timed([&] { k_mix<<<2 * grid, 512>>>(a, b, n, out); }, 5));
     }
+    // producer -> consumer through the Infinity Cache: write a batch of OFDM symbols, then read
+    // it back, batch after batch in one buffer (the fused TX / RX pair at batch granularity)
+    printf(", \"write_then_read_batches\": {");
+    for (size_t mb : {32, 64, 128, 192, 256, 512, 1024}) {
+        const size_t ns = mb * (1u << 20) / 8192;
+        const int reps = (int)(8192 / mb) + 1;
+        const float tw = timed([&] { k_write_sym<false><<<cus * 2, 512>>>((f2*)b, ns, 1.f); }, reps);
+        const float tr = timed([&] { k_read_sym<true><<<cus * 2, 512>>>((const f2*)b, ns, out); }, reps);
+        const float tb = timed([&] {
+            k_write_sym<false><<<cus * 2, 512>>>((f2*)b, ns, 1.f);
+            k_read_sym<true><<<cus * 2, 512>>>((const f2*)b, ns, out);
+        }, reps);
+        const double by = (double)ns * 8192;
+        printf("%s\"%zu MiB\": {\"write_alone\": %.0f, \"read_alone\": %.0f, \"write+read\": %.0f}", mb == 32 ? "" : ", ", mb,
+               by / tw / 1e6, by / tr / 1e6, 2 * by / tb / 1e6);
+    }
+    printf("}");
     printf(", \"write_chunk_oneshot\": %.0f",
            (double)bytes / 1e6 / timed([&] { k_write_chunk<<<(unsigned)((n + 2047) / 2048), 512>>>(b, n, 2.f); }, 5));
     CHECK(hipGetLastError());
