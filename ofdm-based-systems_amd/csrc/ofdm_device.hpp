@@ -691,12 +691,17 @@ __device__ __forceinline__ uint32_t xor3_s(uint32_t a, uint32_t b, uint32_t k) {
     return r;
 }
 
+// OFDM_PHILOX_ROUNDS: diagnostic builds only (timing of the seeding cost); the stream
+// definition is Philox4x32-10
+#ifndef OFDM_PHILOX_ROUNDS
+#define OFDM_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
     // keep the key schedule in the loop (SALU adds next to the VALU rounds): hoisted out of
     // a symbol loop it is 20 live SGPRs and spills
     asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < OFDM_PHILOX_ROUNDS; ++i) {
         // one v_mad_u64_u32 per 32x32->64 product, one v_bitop3 per three-way xor
         const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
         u4 n;

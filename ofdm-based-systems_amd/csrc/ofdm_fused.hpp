@@ -147,6 +147,16 @@ constexpr int rx_waves() {
     return rx_prefetch<FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
 }
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
+// throughput RX: equaliser coefficients staged in LDS up to N = 2^OFDM_EQ_LDS_MAX_LOGN (beyond,
+// the table would cost a resident workgroup per CU)
+#ifndef OFDM_EQ_LDS_MAX_LOGN
+#define OFDM_EQ_LDS_MAX_LOGN 11
+#endif
+#ifndef OFDM_EQ_PRE
+#define OFDM_EQ_PRE 1
+#endif
+template <int FB, int LOGN, int EQ>
+constexpr bool eq_in_lds() { return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= OFDM_EQ_LDS_MAX_LOGN; }
 
 // Reference mode: stage OFDM symbol s's tx bits from the packed bytes of the run
 // (symbol s starts at bit s*bps, zeros past the end) as 32-bit words in W
@@ -654,6 +664,11 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     const int tts_all = FB > 1 && scm ? 2 * TTS : TTS;
     C* tt = cv.take<C>(tts_all);
     OrderParams* ordt = cv.take<OrderParams>(FB == 1 ? 8 : 0);  // adaptive: per-order slicer
+    // throughput kernels with an equaliser: the per-subcarrier coefficient staged in LDS once
+    // per workgroup (ZF: 1/H; MMSE: conj(H), |H|^2 recomputed from it) -- read from the plan's
+    // global table, every element paid an L2 round trip with a vmcnt(0) per symbol
+    constexpr bool EQ_LDS = eq_in_lds<FB, LOGN, EQ>();
+    C* eqt = cv.take<C>(EQ_LDS ? N : 0);
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     const bool noise = a.noise_on && !(a.flags & 1);
@@ -666,6 +681,8 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     build_noise_table(ntab, sigma_d);
     if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
+    if constexpr (EQ_LDS)
+        for (int k = threadIdx.x; k < N; k += BLK) eqt[k] = ((const C*)cm.eq_a)[k];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     if constexpr (FB == 1) {
         if (threadIdx.x < 8) {
@@ -689,6 +706,21 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     uint32_t* W = words + ls * cm.words_per_sym;
     const C* eqa = (const C*)cm.eq_a;
     const R* eqb = (const R*)cm.eq_b;
+    // ZF / MMSE of subcarrier k (equalization/models.py:22-63); nv: the symbol's MMSE noise variance
+    // (pa: the coefficient the throughput kernel preloaded for this element, or null)
+    auto eq_apply = [&](C v, int k, R nv, const C* pa) -> C {
+        if constexpr (EQ_LDS || (FB > 0 && OFDM_EQ_PRE)) {
+            // throughput kernels: ZF 1/H; MMSE conj(H) with |H|^2 recomputed from it
+            const C c = EQ_LDS ? eqt[k] : *pa;
+            if (eq == OFDM_EQ_ZF) return cmul(v, c);
+            const R d = c.re * c.re + c.im * c.im + nv;  // |H|^2 + nv
+            return cscale(cmul(v, c), recip<R>(d));
+        } else {
+            if (eq == OFDM_EQ_ZF) return cmul(v, eqa[k]);
+            if (eq == OFDM_EQ_MMSE) return cmul(v, mmse_coef<R>(eqa[k], eqb[k], nv));
+            return v;
+        }
+    };
     const int cp = cm.cp;
     const R scale = (R)cm.scale;
     Slicer<R> slicer;
@@ -800,6 +832,15 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
 #pragma unroll
             for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
         }
+        // throughput kernels past the LDS table size: the lane's equaliser coefficients are
+        // loaded before the FFT (L2-resident, the same every symbol), so their latency hides
+        // behind it instead of stalling each element of the equaliser
+        constexpr bool EQ_PRE = OFDM_EQ_PRE && FB > 0 && EQ > OFDM_EQ_NONE && !EQ_LDS;
+        C ecoef[EQ_PRE ? E : 1];
+        if constexpr (EQ_PRE) {
+#pragma unroll
+            for (int i = 0; i < E; ++i) ecoef[i] = eqa[t + i * TPS];
+        }
         if (!(a.flags & 2)) fft_reg<R, LOGN, false, (FB > 0)>(x, row, tw, tw + 64, t, tt);
         if (FB == 0) sym_sync<TPS>();  // staged words visible to the whole group
         // MMSE noise variance per OFDM symbol (equalization/models.py:39-49)
@@ -815,13 +856,9 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
         if (scm) {
             // single carrier: equalise every subcarrier, back to time with ifft(ortho)
 #pragma unroll
-            for (int i = 0; i < E; ++i) {
-                const int k = t + i * TPS;
-                if (eq == OFDM_EQ_ZF)
-                    x[i] = cmul(x[i], eqa[k]);
-                else if (eq == OFDM_EQ_MMSE)
-                    x[i] = cmul(x[i], mmse_coef<R>(eqa[k], eqb[k], nv));
-            }
+            for (int i = 0; i < E; ++i)
+                if (eq != OFDM_EQ_NONE)
+                    x[i] = eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_PRE ? i : 0]);
             sym_sync<TPS>();  // the forward FFT has read the row
             if constexpr (FB > 1) {
                 fft_reg<R, LOGN, true, true>(x, row, tw, tw + 64, t, tt + TTS);  // 1/N in the slicer
@@ -836,15 +873,8 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
             const bool all_valid = FB > 1 || sbit + cm.bps <= a.n_valid_bits;
             uint32_t bes = 0, ses = 0;
             auto equalized = [&](int i) {
-                const int k = t + i * TPS;
-                C v = x[i];
-                if (scm) return v;  // single carrier: equalised before the IFFT below
-                if (eq == OFDM_EQ_ZF) {
-                    v = cmul(v, eqa[k]);
-                } else if (eq == OFDM_EQ_MMSE) {
-                    v = cmul(v, mmse_coef<R>(eqa[k], eqb[k], nv));
-                }
-                return v;
+                if (scm || eq == OFDM_EQ_NONE) return x[i];  // single carrier: equalised before the IFFT
+                return eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_PRE ? i : 0]);
             };
             if constexpr (FB == 1) {
                 // four elements per lane word, each through its subcarrier's order (the codes

@@ -10,10 +10,11 @@
 namespace ofdm {
 
 // OFDM_AB_ONLY: experiment builds (Makefile VARIANT=..., tools/ab.sh) instantiate only the
-// N = 1024, 64-QAM kernels of bench configs (b) and (c) -- a minute's compile instead of several
+// N = 1024..4096, 64/256-QAM and adaptive kernels of the bench configs -- a fraction of the
+// full compile
 #ifdef OFDM_AB_ONLY
-#define OFDM_LOGN_CASES(X) X(10)
-#define OFDM_FB_CASES(X) X(6)
+#define OFDM_LOGN_CASES(X) X(10) X(11) X(12)
+#define OFDM_FB_CASES(X) X(6) X(8)
 #else
 #define OFDM_LOGN_CASES(X) \
     X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
@@ -208,7 +209,8 @@ template <typename R, int LOGN, int EQ, int FB>
 static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     constexpr int BLK = rx_block<FB, LOGN, EQ>();
     const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym, FB ? tt_size(LOGN) * (FB > 1 && a.c.scm ? 2 : 1) : 0,
-                                 FB == 1 ? 8 * sizeof(OrderParams) : 0);
+                                 (FB == 1 ? 8 * sizeof(OrderParams) : 0) +
+                                     (eq_in_lds<FB, LOGN, EQ>() ? ((size_t)2 * sizeof(R)) << LOGN : 0));
     auto fn = k_rx<R, LOGN, EQ, FB>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;

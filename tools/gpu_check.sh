@@ -11,6 +11,6 @@ step() {  # name, seconds, command...
     tail -5 "gpurun_out/$name.log"
     case $rc in 0|1) return 0 ;; *) exit $rc ;; esac
 }
-step smoke 300 python __graft_entry__.py smoke
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu ${PYTEST_SECS:-700} python -m pytest tests -m gpu -q -p no:cacheprovider -rf ${PYTEST_ARGS:-}
 step bench ${BENCH_SECS:-240} python bench.py --steps 5 --warmup 1 ${BENCH_ARGS:-}
