@@ -669,6 +669,11 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     // global table, every element paid an L2 round trip with a vmcnt(0) per symbol
     constexpr bool EQ_LDS = eq_in_lds<FB, LOGN, EQ>();
     C* eqt = cv.take<C>(EQ_LDS ? N : 0);
+    // otherwise (throughput kernels at N = 4096, and the complex64 generic kernel) the lane's
+    // coefficients are loaded before the FFT each symbol (L2-resident), so their latency hides
+    // behind it instead of stalling each element of the equaliser
+    constexpr bool EQ_PRE =
+        OFDM_EQ_PRE && !EQ_LDS && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     const bool noise = a.noise_on && !(a.flags & 1);
@@ -709,8 +714,8 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     // ZF / MMSE of subcarrier k (equalization/models.py:22-63); nv: the symbol's MMSE noise variance
     // (pa: the coefficient the throughput kernel preloaded for this element, or null)
     auto eq_apply = [&](C v, int k, R nv, const C* pa) -> C {
-        if constexpr (EQ_LDS || (FB > 0 && OFDM_EQ_PRE)) {
-            // throughput kernels: ZF 1/H; MMSE conj(H) with |H|^2 recomputed from it
+        if constexpr (EQ_LDS || EQ_PRE) {
+            // ZF 1/H; MMSE conj(H) with |H|^2 recomputed from it (complex64 only)
             const C c = EQ_LDS ? eqt[k] : *pa;
             if (eq == OFDM_EQ_ZF) return cmul(v, c);
             const R d = c.re * c.re + c.im * c.im + nv;  // |H|^2 + nv
@@ -832,14 +837,12 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
 #pragma unroll
             for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
         }
-        // throughput kernels past the LDS table size: the lane's equaliser coefficients are
-        // loaded before the FFT (L2-resident, the same every symbol), so their latency hides
-        // behind it instead of stalling each element of the equaliser
-        constexpr bool EQ_PRE = OFDM_EQ_PRE && FB > 0 && EQ > OFDM_EQ_NONE && !EQ_LDS;
         C ecoef[EQ_PRE ? E : 1];
         if constexpr (EQ_PRE) {
+            if (eq != OFDM_EQ_NONE) {
 #pragma unroll
-            for (int i = 0; i < E; ++i) ecoef[i] = eqa[t + i * TPS];
+                for (int i = 0; i < E; ++i) ecoef[i] = eqa[t + i * TPS];
+            }
         }
         if (!(a.flags & 2)) fft_reg<R, LOGN, false, (FB > 0)>(x, row, tw, tw + 64, t, tt);
         if (FB == 0) sym_sync<TPS>();  // staged words visible to the whole group

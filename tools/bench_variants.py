@@ -64,7 +64,7 @@ def adaptive_tables(N, h, snr_db, ser=1e-3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--symbols", type=int, default=1_000_000)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated variant name prefixes (e.g. b,d)")
     args = ap.parse_args()
     only = [o for o in args.only.split(",") if o]
@@ -85,7 +85,10 @@ def main():
                          prefix=B.PREFIX_ZERO if pre == "ZP" else B.PREFIX_CYCLIC,
                          modulator=B.MOD_SC if mod == "SC" else B.MOD_OFDM)
         S = args.symbols if N <= 1024 else args.symbols // (N // 1024)
-        eng.run(S, snr, seed=99)  # warm-up (plan, allocator, clocks)
+        eng.run(S, snr, seed=99)  # warm-up (plan, allocator)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < 0.3:  # clock ramp (bench.py --ramp-seconds)
+            eng.run(S, snr, seed=98)
         torch.cuda.synchronize()
         ev = []
         t0 = time.perf_counter()
