@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace ofdm {
 
 constexpr int kBlock = 256;
@@ -233,6 +235,14 @@ __device__ __forceinline__ void dft(cpx<R>* v) {
     }
 }
 
+template <int I, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < E) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, E>(f);
+    }
+}
+
 // ------------------------------------------------------------------ FFT geometry
 template <int LOGN, int BLK = kBlock>
 struct Geo {
@@ -246,6 +256,14 @@ struct Geo {
 };
 
 __device__ __forceinline__ int pad(int i) { return i + (i >> 4); }
+// pad(b + c) for a constant c that is a multiple of 16: pad(b) + pad(c), so every such
+// access is one base register plus an instruction offset (written as pad(b + c), the
+// compiler materialises and keeps a separate address register per constant)
+template <int C>
+__device__ __forceinline__ int pad_plus(int padded_b) {
+    static_assert(C % 16 == 0, "pad(b + c) = pad(b) + pad(c) needs c = 0 mod 16");
+    return padded_b + C + (C >> 4);
+}
 
 // Per-pass twiddle tables (throughput kernels).  Pass (LOGR, LOGNS > 0) multiplies input r
 // of butterfly k = j mod NS by W^(k r), W = exp(-+2 pi i / (NS RAD)); the tables hold
@@ -385,6 +403,14 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
         static_assert(NB == 1 && STRIDE == G::TPS, "first pass consumes the register layout");
 #pragma unroll
         for (int r = 0; r < RAD; ++r) v[0][r] = x[r];
+    } else if constexpr (G::TPS % 16 == 0 && STRIDE % 16 == 0) {
+        const int pt = pad(t);  // every read is pad(t) + a constant
+        static_for<0, NB>([&](auto Q) {
+            static_for<0, RAD>([&](auto Rr) {
+                v[Q][Rr] = buf[pad_plus<Q * G::TPS + Rr * STRIDE>(pt)];
+            });
+        });
+        if constexpr (!LAST) sym_sync<G::TPS>();  // every read done before the rewrite
     } else {
 #pragma unroll
         for (int q = 0; q < NB; ++q)
@@ -415,6 +441,9 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
         if constexpr (LAST) {
 #pragma unroll
             for (int r = 0; r < RAD; ++r) x[q + r * NB] = v[q][r];
+        } else if constexpr (NS % 16 == 0) {
+            const int pi = pad(((j >> LOGNS) << (LOGNS + LOGR)) + k);
+            static_for<0, RAD>([&](auto Rr) { buf[pad_plus<Rr * NS>(pi)] = v[q][Rr]; });
         } else {
             const int idx = ((j >> LOGNS) << (LOGNS + LOGR)) + k;
 #pragma unroll

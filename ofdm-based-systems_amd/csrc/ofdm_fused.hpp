@@ -294,13 +294,6 @@ __device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm) {
     }
 }
 
-template <int I, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < E) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, E>(f);
-    }
-}
 
 // ============================================================ fused TX
 // Each symbol group walks `chunk` consecutive OFDM symbols so the FIR tail (last L-1
