@@ -3,7 +3,7 @@
 For every SNR point of the sweep (config (c): 0..30 dB in 1 dB steps plus 0.25 dB steps over
 26..29 dB) this runs
 
-* the throughput path (Philox / SFC32 bits and Box-Muller noise generated in the complex64
+* the throughput path (Philox / MWC64X bits and Box-Muller noise generated in the complex64
   kernels), ``--symbols`` OFDM symbols per point, and
 * the reference-stream path (the reference's PCG64 bytes and legacy normals through the
   complex128 kernels -- bit-exact with the reference NumPy code, tests/test_gpu_parity.py),
@@ -40,6 +40,13 @@ CONFIGS = {
     "b": (1024, 64, "flat_fading", "NONE", [float(x) for x in range(0, 31)] + [23.5, 24.25, 24.5, 24.75, 25.25]),
     "c": (1024, 64, "severe_multipath", "MMSE",
           [float(x) for x in range(0, 31)] + [26 + 0.25 * i for i in range(13) if i % 4]),
+    # config (e): 256-QAM, N = 4096, Lin-Phoong P1, MMSE; the 1e-4 crossing is near 38.5 dB
+    "e": (4096, 256, "Lin-Phoong_P1", "MMSE",
+          [float(x) for x in range(20, 43, 2)] + [37.5, 38.0, 38.5, 39.0, 39.5]),
+    # config (d): CAPACITY_BASED loading re-derived at every SNR (orders from water-filling at
+    # that SNR, desired SER 1e-3), so BER does not fall monotonically with SNR: per-point
+    # comparison (no crossing)
+    "d": (2048, 0, "Lin-Phoong_P1", "MMSE", [10.0, 15.0, 20.0, 25.0, 30.0]),
 }
 EQ = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}
 
@@ -76,28 +83,40 @@ def main():
     grid = sorted(set(grid))
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
     cp = len(h) - 1
-    b = int(np.log2(M))
-    lut = [QAMConstellationMapper(M).constellation]
-    e32 = LinkEngine(N, cp, h, EQ[eq], lut, None, B.OFDM_F32)
-    e64 = LinkEngine(N, cp, h, EQ[eq], lut, None, B.OFDM_F64)
+    scale = max(1, N // 1024)  # equal samples per point at any N
+    n_phx, n_ref = args.symbols // scale, max(1, args.ref_symbols // scale)
+    lut = None if M == 0 else [QAMConstellationMapper(M).constellation]
 
+    def engines(snr):
+        if M == 0:  # adaptive: the plan's orders depend on the SNR (bench.make_engine)
+            sys.path.insert(0, ROOT)
+            from bench import make_engine
+
+            cfg = (N, M, ch, 1.0, eq, snr, "")
+            return make_engine(cfg, B.OFDM_F32)[0], make_engine(cfg, B.OFDM_F64)[0]
+        return (LinkEngine(N, cp, h, EQ[eq], lut, None, B.OFDM_F32),
+                LinkEngine(N, cp, h, EQ[eq], lut, None, B.OFDM_F64))
+
+    e32 = e64 = None
     rows = []
     t0 = time.perf_counter()
     for i, snr in enumerate(grid):
         if i % world != rank:
             continue
-        r = e32.run(args.symbols, snr, seed=1000 + i)
-        S = args.ref_symbols if snr >= args.ref_min_snr else max(1, args.ref_symbols // 8)
-        bits = np.random.Generator(np.random.PCG64(i)).bytes(S * N * b // 8)
+        if e32 is None or M == 0:
+            e32, e64 = engines(snr)
+        r = e32.run(n_phx, snr, seed=1000 + i)
+        S = n_ref if snr >= args.ref_min_snr else max(1, n_ref // 8)
+        bits = np.random.Generator(np.random.PCG64(i)).bytes(math.ceil(S * e64.bps / 8))
         rs = np.random.RandomState(i)
         nr = rs.normal(size=S * (N + cp))
         ni = rs.normal(size=S * (N + cp))
         q = e64.run(S, snr, bits=np.frombuffer(bits, np.uint8), normals=(nr, ni))
-        rows.append({"snr_db": snr,
-                     "throughput": {"symbols": args.symbols, "bit_errors": r.bit_errors,
-                                    "ber": r.bit_errors / (args.symbols * N * b)},
+        rows.append({"snr_db": snr, "bits_per_ofdm_symbol": e32.bps,
+                     "throughput": {"symbols": n_phx, "bit_errors": r.bit_errors,
+                                    "ber": r.bit_errors / e32.valid_bits(n_phx)},
                      "reference_streams": {"symbols": S, "bit_errors": q.bit_errors,
-                                           "ber": q.bit_errors / (S * N * b)}})
+                                           "ber": q.bit_errors / e64.valid_bits(S)}})
         print(f"rank {rank}: {snr:6.2f} dB  BER {rows[-1]['throughput']['ber']:.3e} "
               f"(ref streams {rows[-1]['reference_streams']['ber']:.3e})", file=sys.stderr, flush=True)
     if world > 1:
@@ -109,8 +128,13 @@ def main():
     if rank == 0:
         rows.sort(key=lambda x: x["snr_db"])
         snrs = [x["snr_db"] for x in rows]
-        c_phx = crossing(snrs, [x["throughput"]["ber"] for x in rows])
-        c_ref = crossing(snrs, [x["reference_streams"]["ber"] for x in rows])
+        c_phx = crossing(snrs, [x["throughput"]["ber"] for x in rows]) if M else None
+        c_ref = crossing(snrs, [x["reference_streams"]["ber"] for x in rows]) if M else None
+        for x in rows:  # per point: log10 of the BER ratio and its 1-sigma (Poisson counts)
+            et, er = x["throughput"]["bit_errors"], x["reference_streams"]["bit_errors"]
+            if et > 0 and er > 0:
+                x["log10_ber_ratio"] = math.log10(x["throughput"]["ber"] / x["reference_streams"]["ber"])
+                x["log10_ber_ratio_sigma"] = 0.4343 * math.sqrt(1.0 / et + 1.0 / er)
         out = {"config": args.config, "n_fft": N, "qam_order": M, "channel": ch, "cp": cp, "equalizer": eq,
                "n_gpus": world, "wall_s": time.perf_counter() - t0,
                "ber_1e-4_crossing_db": {"throughput": c_phx, "reference_streams": c_ref},
