@@ -20,8 +20,8 @@ Bit / noise sources:
     touches HBM and results do not depend on the number of GPUs.
 
 Multi-GPU: symbols [r*S/R, (r+1)*S/R) go to rank r; the only exchanges are one
-all-reduce of three doubles (the AWGN power is a whole-stream mean,
-noise/models.py:14) and one of the two u64 counters.
+all-gather of three doubles per rank (the AWGN power is a whole-stream mean,
+noise/models.py:14) and one all-reduce of the two u64 counters.
 """
 
 from __future__ import annotations
@@ -171,15 +171,17 @@ class LinkEngine:
         z_out = torch.empty((keep, N), dtype=self.cdtype, device=dev) if keep else None
 
         def reduce_stats():
+            # one collective on the TX -> RX critical path: every rank gathers all ranks'
+            # (sum|y|^2, sum|x|^2, max|x|^2) and reduces them in rank order, so all ranks hold
+            # bit-identical statistics (and sigma)
             if world > 1:
                 import torch.distributed as dist
 
-                s01 = stats[:2].clone()
-                dist.all_reduce(s01, op=dist.ReduceOp.SUM, group=group)
-                pk = stats[2:].clone()
-                dist.all_reduce(pk, op=dist.ReduceOp.MAX, group=group)
-                stats[:2].copy_(s01)
-                stats[2:].copy_(pk)
+                parts = [torch.empty_like(stats) for _ in range(world)]
+                dist.all_gather(parts, stats, group=group)
+                g = torch.stack(parts)
+                stats[:2].copy_(g[:, :2].sum(0))
+                stats[2:].copy_(g[:, 2:].amax(0))
 
         if per_batch >= mine:
             # whole shard resident: one TX, one RX
