@@ -9,9 +9,10 @@
 // wavefront and every synchronisation is wave-local (sym_sync), so the 4 waves of a
 // workgroup run decoupled.
 //
-// Specialisations: FB = 2/4/6/8 selects the throughput kernel (fixed square QAM with
-// b = FB bits, Philox-keyed bits and noise, complex64; OFDM or SC-OFDM, cyclic prefix or
-// zero padding as wave-uniform run-time flags); FB = 1 is the throughput kernel for adaptive
+// Specialisations: FB = 2/4/6/8 selects the throughput kernel (fixed square QAM -- or the
+// reference's 4/16-PSK -- with b = FB bits, Philox-keyed bits and noise, complex64; OFDM or
+// SC-OFDM, cyclic prefix or zero padding as wave-uniform run-time flags); FB = 3/5 the same
+// kernel for the reference's 8/32-PSK (sector decisions only); FB = 1 is the throughput kernel for adaptive
 // bit loading (per-subcarrier square-QAM orders, CAPACITY_BASED, OFDM with a cyclic prefix);
 // FB = 0 is the generic kernel (reference-mode bytes and normals, PSK, complex128, adaptive
 // SC-OFDM / zero padding).
@@ -642,6 +643,8 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     const bool zp = FB == 1 ? false : (bool)cm.zpad;  // zero-padding guard (run-time, uniform)
     const bool nn = FB ? false : (bool)cm.nn;
     const int ystride = FB == 1 ? N : cm.ystride;
+    // odd bits per subcarrier (FB = 3, 5): the reference's 8- / 32-PSK only
+    constexpr bool FB_PSK_ONLY = FB > 1 && (FB & 1);
     // noise phase table: static LDS at a link-time constant address, so a lane word's bits 3..8
     // (its byte offset) address an entry with no add
     __shared__ f32x2 ntab[kNoisePhases];
@@ -737,7 +740,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
             }
             ocode[q] = w;
         }
-    } else if constexpr (FB > 1) {
+    } else if constexpr (FB > 1 && !FB_PSK_ONLY) {
         // the FFT output stays unscaled (x sqrt N); SC-OFDM adds the unscaled IFFT (x sqrt N).
         // The reference's 4/16-PSK (psk_m > 0) decide by sector and have no axis tables.
         if (cm.psk_m == 0) pslicer.load(axis[0], (float)(scm ? cm.scale * cm.scale : cm.scale));
@@ -911,15 +914,16 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
                     C z[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
-                    uint32_t d;
-                    // the reference's M-PSK (M <= 32 with even b: 4- and 16-PSK): sector
+                    uint32_t d = 0;
+                    // the reference's M-PSK (M <= 32: 4- and 16-PSK share the QAM kernels'
+                    // FB = 2 / 4, 8- and 32-PSK have FB = 3 / 5 to themselves): sector
                     // decisions (psk_decide); compiled out of the 64/256-QAM kernels
-                    if (FB <= 4 && cm.psk_m > 0) {
+                    if (FB_PSK_ONLY || (FB <= 4 && cm.psk_m > 0)) {
                         uint32_t r = 0;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) r |= psk_decide(z[j], cm) << (8 * j);
                         d = r ^ (lane_word(tb.lane, q) & PermSlicer<FB>::BYTE_MASK);
-                    } else {
+                    } else if constexpr (!FB_PSK_ONLY) {
                         d = pslicer.diff(z, lane_word(tb.lane, q));
                     }
                     bes += __popc(d);

@@ -18,7 +18,7 @@ namespace ofdm {
 #else
 #define OFDM_LOGN_CASES(X) \
     X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
-#define OFDM_FB_CASES(X) X(2) X(4) X(6) X(8)
+#define OFDM_FB_CASES(X) X(2) X(3) X(4) X(5) X(6) X(8)
 #endif
 
 template <typename F>
@@ -169,7 +169,7 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     return tx_launch<R, LOGN, FB, -1>(a, grid, s);
 }
 
-// Throughput configuration (complex64, fixed square QAM or the reference's 4/16-PSK (psk_m > 0),
+// Throughput configuration (complex64, fixed square QAM or the reference's 4/8/16/32-PSK (psk_m > 0),
 // Philox bits; N >= 64; OFDM or SC-OFDM, cyclic prefix or zero padding) -> the kernel specialised on the bits per
 // subcarrier; adaptive bit loading over the reference's square-QAM LUTs (OFDM, cyclic
 // prefix) -> the adaptive throughput kernel (FB = 1); anything else -> the generic kernel.
@@ -178,7 +178,8 @@ static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
             return tx_fast<R, LOGN, 1>(a, grid, s);
-        if (!a.c.adaptive && a.c.bits == nullptr && (!a.c.nn || a.c.psk_m > 0)) {  // OFDM / SC, CP / ZP, QAM / PSK
+        // OFDM / SC, CP / ZP, QAM / PSK (odd bits: the reference's 8/32-PSK only)
+        if (!a.c.adaptive && a.c.bits == nullptr && (!a.c.nn || a.c.psk_m > 0) && (a.c.b % 2 == 0 || a.c.psk_m > 0)) {
 #define OFDM_TX_FB(F) \
     case F:              \
         return tx_fast<R, LOGN, F>(a, grid, s);
@@ -227,7 +228,7 @@ static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
     return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB>(a, grid, s);
 }
 
-// Throughput configuration (complex64, fixed square QAM or the reference's 4/16-PSK (psk_m > 0),
+// Throughput configuration (complex64, fixed square QAM or the reference's 4/8/16/32-PSK (psk_m > 0),
 // Philox bits and noise, no received-symbol tap; N >= 64) -> kernel specialised on bits and
 // equaliser; anything else -> the generic kernel.
 template <typename R, int LOGN>
@@ -237,7 +238,7 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
             !a.c.scm && !a.c.zpad && !a.c.nn)
             return rx_eq<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
-            (!a.c.nn || a.c.psk_m > 0)) {  // OFDM / SC, CP / ZP, QAM / PSK
+            (!a.c.nn || a.c.psk_m > 0) && (a.c.b % 2 == 0 || a.c.psk_m > 0)) {  // OFDM / SC, CP / ZP, QAM / PSK
 #define OFDM_RX_FB(F) \
     case F:              \
         return rx_eq<R, LOGN, F>(a, grid, s);

@@ -63,6 +63,10 @@ CASES = [
     (128, 4, "severe_multipath", "ZF", 1024, 10.0, B.OFDM_F32, {"scheme": "PSK", "prefix": "ZP"}),
     (256, 16, "two_ray", "MMSE", 256, 18.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC"}),
     (512, 4, "Lin-Phoong_P1", "MMSE", 256, 9.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC"}),
+    # 8- and 32-PSK (odd bits) on their own throughput kernels (FB = 3 / 5), with SC-OFDM and
+    # zero padding; (256, 8, ...) and (512, 32, ...) above cover plain OFDM
+    (1024, 8, "Lin-Phoong_P2", "MMSE", 128, 22.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC", "prefix": "ZP"}),
+    (256, 32, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F32, {"scheme": "PSK", "prefix": "ZP"}),
     # CAPACITY_BASED bit loading (config d): per-subcarrier orders from water-filling at the SNR;
     # an odd symbol count leaves a trailing partial byte that is not compared
     (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F32, {"adaptive": True}),
