@@ -265,15 +265,18 @@ hipError_t launch_rx(int logn, const RxArgs& a, int* grid, hipStream_t s) {
 #undef OFDM_RX_CASE
 }
 
-#define OFDM_INSTANTIATE(R)                                                         \
+// The launchers are instantiated in three groups so the complex64 kernels -- the bulk of
+// the compile -- build as separate translation units in parallel (ofdm_kernels_f32*.hip).
+#define OFDM_INSTANTIATE_OPS(R)                                                     \
     template hipError_t launch_rows<R>(int, int, const RowsArgs&, hipStream_t);     \
     template hipError_t launch_equalize<R>(const EqArgs&, hipStream_t);             \
     template hipError_t launch_map<R>(const MapArgs&, hipStream_t);                 \
     template hipError_t launch_demap<R>(const DemapArgs&, hipStream_t);             \
     template hipError_t launch_conv<R>(const ConvArgs&, int, hipStream_t);          \
     template hipError_t launch_power<R>(const PowerArgs&, int, hipStream_t);        \
-    template hipError_t launch_awgn<R>(const AwgnArgs&, hipStream_t);               \
-    template hipError_t launch_tx<R>(int, const TxArgs&, int*, hipStream_t);         \
-    template hipError_t launch_rx<R>(int, const RxArgs&, int*, hipStream_t);
+    template hipError_t launch_awgn<R>(const AwgnArgs&, hipStream_t);
+#define OFDM_INSTANTIATE_TX(R) template hipError_t launch_tx<R>(int, const TxArgs&, int*, hipStream_t);
+#define OFDM_INSTANTIATE_RX(R) template hipError_t launch_rx<R>(int, const RxArgs&, int*, hipStream_t);
+#define OFDM_INSTANTIATE(R) OFDM_INSTANTIATE_OPS(R) OFDM_INSTANTIATE_TX(R) OFDM_INSTANTIATE_RX(R)
 
 }  // namespace ofdm
