@@ -67,6 +67,8 @@ CASES = [
     # zero padding; (256, 8, ...) and (512, 32, ...) above cover plain OFDM
     (1024, 8, "Lin-Phoong_P2", "MMSE", 128, 22.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC", "prefix": "ZP"}),
     (256, 32, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F32, {"scheme": "PSK", "prefix": "ZP"}),
+    (64, 8, "rayleigh_fading", "ZF", 2048, 20.0, B.OFDM_F32, {"scheme": "PSK", "prefix": "ZP"}),  # 4 lanes/symbol
+    (128, 32, "two_ray", "MMSE", 1024, 26.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC"}),
     # CAPACITY_BASED bit loading (config d): per-subcarrier orders from water-filling at the SNR;
     # an odd symbol count leaves a trailing partial byte that is not compared
     (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F32, {"adaptive": True}),
