@@ -1,0 +1,45 @@
+"""bench.py's measurement definitions on CPU: the algorithmic bytes per OFDM symbol against
+SURVEY.md 8(d)'s worked values, the configs against BASELINE.json, and the adaptive config's
+bit loading (built exactly as Simulation builds it)."""
+
+import json
+import os
+
+import numpy as np
+from conftest import ROOT
+
+import bench
+
+
+def test_algorithmic_bytes_match_the_survey():
+    # B_alg = 2 ceil(bps / 8) + 2 (N + cp) 8 per symbol, split evenly over TX / RX;
+    # worked values (b) 17 920 B, (c) 18 032 B, (e) 1024 b + 65 584 B at b = 8
+    assert 2 * bench.kernel_bytes_per_symbol(1024, 1024 * 6, 0) == 17920
+    assert 2 * bench.kernel_bytes_per_symbol(1024, 1024 * 6, 7) == 18032
+    assert 2 * bench.kernel_bytes_per_symbol(4096, 4096 * 8, 3) == 1024 * 8 + 65584
+
+
+def test_configs_follow_baseline():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert "N_FFT=1024 64-QAM" in base["metric"]
+    N, M, ch, ratio, eq, snr, _ = bench.CONFIGS["b"]  # configs[1]: AWGN only, one SNR
+    assert (N, M, ch, eq) == (1024, 64, "flat_fading", "NONE")
+    N, M, ch, ratio, eq, snr, _ = bench.CONFIGS["c"]  # configs[2]: custom multipath + MMSE
+    assert (N, M, ch, eq) == (1024, 64, "severe_multipath", "MMSE")
+    N, M, ch, ratio, eq, snr, _ = bench.CONFIGS["d"]  # configs[3]: adaptive, N = 2048
+    assert (N, M, eq) == (2048, 0, "MMSE")
+    N, M, ch, ratio, eq, snr, _ = bench.CONFIGS["e"]  # configs[4]: N = 4096, up to 256-QAM
+    assert (N, M, eq) == (4096, 256, "MMSE")
+    for cfg in bench.CONFIGS.values():
+        assert os.path.exists(os.path.join(ROOT, "config", "channel_models", cfg[2] + ".npy"))
+
+
+def test_adaptive_config_orders_follow_the_reference_rule():
+    import ofdm_oracle as O
+
+    N, M, ch, ratio, eq, snr, _ = bench.CONFIGS["d"]
+    h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+    orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
+    bps = sum(int(np.log2(o)) for o in orders if o > 0)
+    assert 0 < bps < 8 * N and all(o == 0 or (o & (o - 1)) == 0 for o in orders)
