@@ -595,8 +595,10 @@ struct PermSlicer {
 // is taken on -Im z, both axes look up U, and the Q bits move up by b_k/2.
 constexpr uint32_t kUPat[4] = {0x02030100u, 0x05040607u, 0x0D0C0E0Fu, 0x0A0B0908u};
 
-// byte j of the result = U[byte j of sel] (bytes of sel < 16)
+// byte j of the result = U[byte j of sel] (bytes of sel < 16; SMALL: < 8, orders <= 64)
+template <bool SMALL = false>
 __device__ __forceinline__ uint32_t upat_lookup(uint32_t sel) {
+    if constexpr (SMALL) return __builtin_amdgcn_perm(kUPat[1], kUPat[0], sel);
     const uint32_t s7 = sel & 0x07070707u;
     const uint32_t lo = __builtin_amdgcn_perm(kUPat[1], kUPat[0], s7);
     const uint32_t hi = __builtin_amdgcn_perm(kUPat[3], kUPat[2], s7);
@@ -614,17 +616,27 @@ struct OrderParams {
 constexpr int kUnusedOrder = 7;
 
 // (rx ^ tx) of four elements of possibly different orders, one per byte.  op[j] = the
-// element's order entry, txw = the lane word; mask_out = the tx masks (byte j).
+// element's order entry, txw = the lane word; mask_out = the tx masks (byte j).  SMALL: every
+// order of the plan is <= 64 (levels < 8: one v_perm per U lookup).
+template <bool SMALL>
 __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], const OrderParams* const (&op)[4],
                                                   uint32_t txw) {
     constexpr int MAGIC = 0x4B400000;  // bit pattern of 1.5 * 2^23: round(y) in the low mantissa
     uint32_t li[4], lq[4], meta[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const float mul = op[j]->mul, add = op[j]->add;
-        // level coordinates Re z * mul + add and -Im z * mul + add
-        const float fx = __builtin_fmaf(z[j].re, mul, add) + 12582912.0f;
-        const float fy = __builtin_fmaf(-z[j].im, mul, add) + 12582912.0f;
+        // level coordinates (Re z * mul + add, -Im z * mul + add) in one v_pk_fma_f32: (mul, add)
+        // is one register pair, splatted / negated by the operand modifiers (written in C the
+        // two axes' chains were merged -- the Q axis vanished from the ISA).
+        // The result is taken as a 64-bit integer: read back as a float2 whose lanes are then
+        // bit-cast, the compiler used lane 0 for both (reproduced in a 15-line kernel)
+        const f32x2 ma = *(const f32x2*)&op[j]->mul;
+        uint64_t f;
+        asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
+            : "=v"(f)
+            : "v"(z[j].v), "v"(ma));
+        const float fx = __builtin_bit_cast(float, (uint32_t)f) + 12582912.0f;
+        const float fy = __builtin_bit_cast(float, (uint32_t)(f >> 32)) + 12582912.0f;
         const int smax = (int)op[j]->smax;
         li[j] = (uint32_t)min(max(__builtin_bit_cast(int, fx), MAGIC), smax);
         lq[j] = (uint32_t)min(max(__builtin_bit_cast(int, fy), MAGIC), smax);
@@ -637,7 +649,7 @@ __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], cons
                                               __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
     const uint32_t sq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(lq[3], lq[2], 0x0c0c0400u),
                                               __builtin_amdgcn_perm(lq[1], lq[0], 0x0c0c0400u), 0x05040100u);
-    const uint32_t ib = upat_lookup(si), qb = upat_lookup(sq);
+    const uint32_t ib = upat_lookup<SMALL>(si), qb = upat_lookup<SMALL>(sq);
     // Q bits << b_j/2 per byte: bytes 0, 2 and 1, 3 as u16 pairs through v_pk_mul_lo_u16
     typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     const uint32_t w02 = __builtin_amdgcn_perm(0u, qb, 0x0c020c00u), w13 = __builtin_amdgcn_perm(0u, qb, 0x0c030c01u);

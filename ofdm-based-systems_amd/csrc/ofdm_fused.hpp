@@ -729,7 +729,11 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     // adaptive throughput kernel: the LDS byte offset of each element's order entry, four
     // elements per word (the lane's subcarriers do not change from symbol to symbol)
     uint32_t ocode[FB == 1 ? E / 4 : 1];
+    bool small_orders = false;  // adaptive: every order <= 64 (3-bit levels)
     if constexpr (FB == 1) {
+        int side = 0;
+        for (int l = 0; l < cm.n_axis; ++l) side = max(side, (int)axis[l].side);
+        small_orders = side <= 8;
 #pragma unroll
         for (int q = 0; q < E / 4; ++q) {
             uint32_t w = 0;
@@ -889,7 +893,8 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
                         z[j] = equalized(4 * q + j);
                         op[j] = (const OrderParams*)((const unsigned char*)ordt + ((oc >> (8 * j)) & 0xFFu));
                     }
-                    uint32_t d = adaptive_diff(z, op, lane_word(tb.lane, q));
+                    uint32_t d = small_orders ? adaptive_diff<true>(z, op, lane_word(tb.lane, q))
+                                              : adaptive_diff<false>(z, op, lane_word(tb.lane, q));
                     ses += PermSlicer<8>::nonzero_bytes(d);
                     if (!all_valid) {
                         // a trailing partial byte of the run is not compared (constellation/
