@@ -1,0 +1,73 @@
+"""Size-independent properties of the throughput path at the benchmark's full sizes
+(BASELINE configs (b) and (e): 1e6 OFDM symbols of N = 1024, 2.5e5 of N = 4096 -- 8.2 GB of
+channel samples per launch), where the oracle cannot follow:
+
+* a noise-free link decodes every bit (map -> IFFT -> channel -> FFT -> equaliser -> slicer
+  are exact inverses up to float rounding far below the decision distance);
+* error counts are additive: one RX launch over [0, S) counts exactly what two RX launches over
+  [0, S/2) and [S/2, S) count with the same TX statistics (sigma from the whole stream);
+* results do not depend on batching: the batched schedule (power pass, then TX+RX per batch)
+  gives the counts of the single-launch schedule.
+"""
+
+import numpy as np
+import pytest
+import torch
+from conftest import channel
+
+import ofdm_oracle as O
+from ofdm_based_systems import _backend as B
+from ofdm_based_systems.engine import LinkEngine
+
+pytestmark = pytest.mark.gpu
+
+FULL = [  # N, M, channel, equaliser, symbols, SNR dB
+    (1024, 64, "flat_fading", B.EQ_NONE, 1_000_000, 24.0),
+    (4096, 256, "Lin-Phoong_P1", B.EQ_MMSE, 250_000, 34.0),
+]
+
+
+def _engine(N, M, ch, eq):
+    h = channel(ch)
+    return LinkEngine(N, len(h) - 1, h, eq, [O.qam_lut(M)], None, B.OFDM_F32)
+
+
+@pytest.mark.parametrize("N,M,ch,eq,S,snr", FULL, ids=["b", "e"])
+def test_full_size_noise_free_is_error_free(gpu, N, M, ch, eq, S, snr):
+    eng = _engine(N, M, ch, eq)
+    r = eng.run(S, snr, seed=3, noise_on=False)
+    assert r.bit_errors == 0 and r.symbol_errors == 0
+    assert 0.9 < r.power_sum / r.samples < 1.1  # unit-power constellation, unit-power channel
+    assert 8.0 < r.papr_db < 14.0
+
+
+@pytest.mark.parametrize("N,M,ch,eq,S,snr", FULL, ids=["b", "e"])
+def test_full_size_counts_are_additive(gpu, N, M, ch, eq, S, snr):
+    eng = _engine(N, M, ch, eq)
+    st = eng.stream()
+    y = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
+    stats = torch.zeros(3, dtype=torch.float64, device="cuda")
+    eng.tx(st, None, 7, 0, S, y, stats)
+    samples = S * (N + eng.cp)
+    whole = torch.zeros(2, dtype=torch.int64, device="cuda")
+    eng.rx(st, y, None, None, 7, stats, samples, snr, 1, None, 0, S, eng.valid_bits(S), whole)
+    parts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    h = S // 2
+    eng.rx(st, y[:h], None, None, 7, stats, samples, snr, 1, None, 0, h, eng.valid_bits(S), parts)
+    eng.rx(st, y[h:], None, None, 7, stats, samples, snr, 1, None, h, S - h, eng.valid_bits(S), parts)
+    torch.cuda.synchronize()
+    w, p = whole.cpu().numpy(), parts.cpu().numpy()
+    assert w[0] > 1000 and np.array_equal(w, p), (w, p)
+    # and the same run through the engine's own schedule
+    r = eng.run(S, snr, seed=7)
+    assert (r.bit_errors, r.symbol_errors) == (int(w[0]), int(w[1]))
+
+
+def test_full_size_batching_invariance(gpu):
+    N, M, ch, eq, S, snr = FULL[0]
+    eng = _engine(N, M, ch, eq)
+    a = eng.run(S, snr, seed=21)
+    b = eng.run(S, snr, seed=21, batch=250_000)
+    assert a.bit_errors > 1000
+    assert (a.bit_errors, a.symbol_errors) == (b.bit_errors, b.symbol_errors)
+    assert a.power_sum == pytest.approx(b.power_sum, rel=1e-12)
