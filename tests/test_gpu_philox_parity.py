@@ -69,6 +69,11 @@ CASES = [
     (256, 32, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F32, {"scheme": "PSK", "prefix": "ZP"}),
     (64, 8, "rayleigh_fading", "ZF", 2048, 20.0, B.OFDM_F32, {"scheme": "PSK", "prefix": "ZP"}),  # 4 lanes/symbol
     (128, 32, "two_ray", "MMSE", 1024, 26.0, B.OFDM_F32, {"scheme": "PSK", "modulator": "SC"}),
+    # prefix shorter than the channel (prefix_length_ratio < 1): inter-symbol interference
+    # through the FIR's tail of the previous symbol; no prefix at all on a 4-tap channel
+    (256, 16, "severe_multipath", "MMSE", 512, 16.0, B.OFDM_F32, {"cp": 2}),
+    (1024, 64, "Lin-Phoong_P2", "MMSE", 256, 30.0, B.OFDM_F32, {"cp": 1}),
+    (512, 4, "default_multipath", "ZF", 512, 12.0, B.OFDM_F32, {"cp": 0}),
     # CAPACITY_BASED bit loading (config d): per-subcarrier orders from water-filling at the SNR;
     # an odd symbol count leaves a trailing partial byte that is not compared
     (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F32, {"adaptive": True}),
@@ -92,7 +97,7 @@ def setup(N, M, ch, eq, prec, var=None, snr=None):
     """Engine of a case; returns (engine, CIR, cp, keyword arguments for P.run_philox)."""
     var = dict(var or {})
     h = channel(ch)
-    cp = len(h) - 1
+    cp = var.pop("cp", len(h) - 1)
     sc = None
     if var.pop("adaptive", False):
         orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
