@@ -203,28 +203,37 @@ class LinkEngine:
                 zk = keep if b0 == lo else 0
                 self.rx(stream, y, nr_d, ni_d, seed, stats, samples, snr_db, noise_on, bits_d, b0, nb,
                         n_valid, counters, z_out if zk else None, zk)
+        work = None
         if world > 1:
             import torch.distributed as dist
 
-            dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group)
+            # off the critical path: the next run's TX does not wait for this reduction;
+            # result() waits for it before reading the counters
+            work = dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group, async_op=True)
         done = None
         if dev.type == "cuda":
             done = torch.cuda.Event()
             done.record()  # on the launch stream: result() may be called under another stream
-        return PendingLink(n_sym, samples, stats, counters, z_out, done)
+        return PendingLink(n_sym, samples, stats, counters, z_out, done, work)
 
 
 class PendingLink:
     """Device-side results of one :meth:`LinkEngine.run_async` call."""
 
-    def __init__(self, n_sym, samples, stats, counters, z_out, done=None):
+    def __init__(self, n_sym, samples, stats, counters, z_out, done=None, work=None):
         self.n_sym, self.samples = n_sym, samples
         self.stats, self.counters, self.z_out = stats, counters, z_out
         self.done = done
+        self.work = work  # the asynchronous counter all-reduce (multi-rank), or None
 
     def result(self) -> LinkStats:
         if self.done is not None:
             self.done.synchronize()
+        if self.work is not None:
+            self.work.wait()  # the reduced counters (host-blocking for gloo, stream-ordered for RCCL)
+            self.work = None
+            if self.counters.is_cuda:
+                torch.cuda.current_stream().synchronize()
         st = self.stats.cpu().numpy()
         cnt = self.counters.cpu().numpy()
         samples = self.samples
