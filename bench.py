@@ -245,9 +245,10 @@ def main():
     events = []
     bit_errors = 0
     t0 = time.perf_counter()
-    # every step is the whole hot path (bits -> ... -> error counts); the host enqueues
-    # step k+1 while the GPU runs step k and reads all counts back inside the timed region
-    pending = [engine.run_async(total, snr, seed=k, group=group, events=events) for k in range(args.steps)]
+    # every step is the whole hot path (bits -> ... -> error counts) of one run; the host
+    # enqueues all steps (step k+1's TX ahead of step k's RX, so the ranks' statistics
+    # exchange overlaps a transmitter) and reads every run's counts back inside the timed region
+    pending = engine.run_pipelined(total, snr, range(args.steps), group=group, events=events)
     for p in pending:
         bit_errors += p.result().bit_errors
     torch.cuda.synchronize()

@@ -217,6 +217,69 @@ class LinkEngine:
         return PendingLink(n_sym, samples, stats, counters, z_out, done, work)
 
 
+    def run_pipelined(self, n_sym: int, snr_db: float, seeds, *, group=None,
+                      events: Optional[list] = None) -> list:
+        """Independent throughput-mode runs (one per seed) of global OFDM symbols [0, n_sym),
+        software-pipelined across runs: run k+1's TX is enqueued before run k's RX, so with
+        several ranks the statistics exchange of run k (the one collective on a run's
+        TX -> RX path) is in flight while the GPU transmits run k+1.  Every run is complete
+        and its counts are those of :meth:`run_async` with the same seed; returns the
+        PendingLink of each run."""
+        dev = self.device()
+        stream = self.stream()
+        world, rank = 1, 0
+        if group is not None:
+            import torch.distributed as dist
+
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+        lo, hi = shard(n_sym, rank, world)
+        mine = hi - lo
+        N, cp = self.n_fft, self.cp
+        samples = n_sym * (N + cp)
+        n_valid = self.valid_bits(n_sym)
+
+        def tx(seed):
+            stats = torch.zeros(3, dtype=torch.float64, device=dev)
+            y = torch.empty((max(mine, 1), self.ystride), dtype=self.cdtype, device=dev)
+            self._timed(events, "ofdm_tx", mine, lambda: self.tx(stream, None, seed, lo, mine, y, stats))
+            work = None
+            if world > 1:
+                import torch.distributed as dist
+
+                parts = [torch.empty_like(stats) for _ in range(world)]
+                work = (dist.all_gather(parts, stats, group=group, async_op=True), parts)
+            return seed, y, stats, work
+
+        def rx(state):
+            seed, y, stats, work = state
+            if work is not None:  # reduce the gathered statistics in rank order (as run_async)
+                work[0].wait()
+                g = torch.stack(work[1])
+                stats[:2].copy_(g[:, :2].sum(0))
+                stats[2:].copy_(g[:, 2:].amax(0))
+            counters = torch.zeros(2, dtype=torch.int64, device=dev)
+            self._timed(events, "ofdm_rx", mine, lambda: self.rx(
+                stream, y, None, None, seed, stats, samples, snr_db, True, None, lo, mine, n_valid, counters))
+            red = None
+            if world > 1:
+                import torch.distributed as dist
+
+                red = dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group, async_op=True)
+            done = torch.cuda.Event() if dev.type == "cuda" else None
+            if done is not None:
+                done.record()
+            return PendingLink(n_sym, samples, stats, counters, None, done, red)
+
+        seeds = list(seeds)
+        out = []
+        cur = tx(seeds[0]) if seeds else None
+        for k in range(len(seeds)):
+            nxt = tx(seeds[k + 1]) if k + 1 < len(seeds) else None
+            out.append(rx(cur))
+            cur = nxt
+        return out
+
+
 class PendingLink:
     """Device-side results of one :meth:`LinkEngine.run_async` call."""
 

@@ -35,8 +35,16 @@ class OracleEngine(LinkEngine):
         self.hn = O.normalize_h(self.h)
         self.H = np.fft.fft(self.h, N)
 
+        self.streams = {}  # seed -> (bits, nr, ni) standing in for the in-kernel streams
+
     def device(self):
         return torch.device("cpu")
+
+    def seed_streams(self, seed, S):
+        """Throughput-mode stand-in: the double's 'in-kernel' bits and noise of a seed."""
+        tx, nz = O.reference_streams(seed, S * self.bps, S * (self.n_fft + self.cp))
+        self.streams[seed] = (torch.from_numpy(np.frombuffer(tx, np.uint8).copy()),
+                              torch.from_numpy(nz[0]), torch.from_numpy(nz[1]))
 
     def stream(self):
         return None
@@ -52,6 +60,8 @@ class OracleEngine(LinkEngine):
         return O.add_cp(np.fft.ifft(X[None, :], norm="ortho"), cp)[0]
 
     def tx(self, stream, bits_d, seed, sym0, n_sym, y, stats):
+        if bits_d is None:
+            bits_d = self.streams[seed][0]
         L = len(self.h)
         for s in range(sym0, sym0 + n_sym):
             ext = self._ext(bits_d, s)
@@ -66,6 +76,8 @@ class OracleEngine(LinkEngine):
     def rx(self, stream, y, nr, ni, seed, stats, total_samples, snr_db, noise_on, bits_d, sym0, n_sym,
            n_valid, counters, z_out=None, z_keep=0):
         N, cp = self.n_fft, self.cp
+        if bits_d is None:
+            bits_d, nr, ni = self.streams[seed]
         sigma = np.sqrt(float(stats[0]) / total_samples / 10 ** (snr_db / 10) / 2) if noise_on else 0.0
         nb = self.bps // 8
         for s in range(sym0, sym0 + n_sym):
@@ -123,6 +135,41 @@ def test_sharded_engine_matches_single_process_oracle(world, batch):
         assert (be, se) == (ref.bit_errors, ref.symbol_errors), (r, be, se, ref)
         assert abs(papr - ref.papr_db) < 1e-9
     assert len({out[r][3] for r in range(world)}) == 1  # every rank saw the same global power
+
+
+def _pipelined_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = CASE
+    h = channel(c["ch"])
+    eng = OracleEngine(c["N"], c["M"], h, len(h) - 1, c["eq"])
+    seeds = [11, 12, 13]
+    for sd in seeds:
+        eng.seed_streams(sd, c["S"])
+    piped = [p.result() for p in eng.run_pipelined(c["S"], c["snr"], seeds, group=dist.group.WORLD)]
+    serial = [eng.run(c["S"], c["snr"], seed=sd, group=dist.group.WORLD) for sd in seeds]
+    out[rank] = ([(r.bit_errors, r.symbol_errors, r.power_sum) for r in piped],
+                 [(r.bit_errors, r.symbol_errors, r.power_sum) for r in serial])
+    dist.destroy_process_group()
+
+
+def test_pipelined_runs_match_serial_runs():
+    """bench.py's schedule (run k+1's TX enqueued before run k's RX, asynchronous exchanges)
+    gives every run the counts and statistics of LinkEngine.run with the same seed, on every
+    rank, and those of the single-process oracle."""
+    c = CASE
+    h = channel(c["ch"])
+    cp = len(h) - 1
+    b = int(np.log2(c["M"]))
+    out = mp.Manager().dict()
+    mp.spawn(_pipelined_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        piped, serial = out[r]
+        assert piped == serial, (r, piped, serial)
+    for k, sd in enumerate([11, 12, 13]):
+        tx, nz = O.reference_streams(sd, c["S"] * c["N"] * b, c["S"] * (c["N"] + cp))
+        ref = O.run_fixed(tx, c["S"] * c["N"] * b, c["N"], c["M"], h, cp, c["eq"], c["snr"], nz)
+        assert out[0][0][k][:2] == (ref.bit_errors, ref.symbol_errors)
 
 
 def test_shard_covers_range_exactly():
