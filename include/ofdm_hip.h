@@ -166,8 +166,9 @@ int ofdm_power(ofdm_plan_t plan, void* stream, const void* y, int64_t len, doubl
  * Bit source: `bits` != NULL -> packed tx bytes of the WHOLE run (OFDM symbol s
  * starts at bit s*bits_per_ofdm_symbol), e.g. the reference's PCG64 bytes
  * (parity mode).  bits == NULL -> throughput mode: bits and noise from the
- * counter-based lane streams keyed by (seed, global symbol) (Philox4x32-10 seeding
- * SFC32; definition in csrc/ofdm_device.hpp, restated in oracle/philox_streams.py).
+ * counter-based lane streams keyed by (seed, global symbol) (stream version 2:
+ * Philox4x32-10 seeding MWC64X; definition in csrc/ofdm_device.hpp, restated in
+ * oracle/philox_streams.py).  n_sym = 0 is an empty call (returns 0, launches nothing).
  *
  * ofdm_tx: for global OFDM symbols [sym0, sym0+n_sym): map -> IFFT(ortho) (OFDM) or
  *   nothing (single carrier) -> cyclic prefix or zero guard -> linear convolution with

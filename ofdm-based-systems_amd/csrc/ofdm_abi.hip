@@ -697,10 +697,10 @@ int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const 
     if (!p || !p->has_const) return fail(OFDM_E_INVALID, "ofdm_rx needs a constellation");
     if (!p->separable && p->adaptive) return fail(OFDM_E_INVALID, "adaptive loading needs square-QAM constellations");
     if (p->eq != OFDM_EQ_NONE && !p->has_channel) return fail(OFDM_E_INVALID, "plan has no channel response");
-    if (n_sym < 0 || sym0 < 0 || !counters || (n_sym > 0 && !y) || (noise_on && (!stats || total_samples <= 0)))
-        return fail(OFDM_E_INVALID, "bad argument to ofdm_rx");
+    if (n_sym < 0 || sym0 < 0 || !counters) return fail(OFDM_E_INVALID, "bad argument to ofdm_rx");
+    if (n_sym == 0) return OFDM_OK;  // an empty run (its stream has no samples and no noise power)
+    if (!y || (noise_on && (!stats || total_samples <= 0))) return fail(OFDM_E_INVALID, "bad argument to ofdm_rx");
     if ((nr == nullptr) != (ni == nullptr)) return fail(OFDM_E_INVALID, "nr and ni must both be given or both NULL");
-    if (n_sym == 0) return OFDM_OK;
     RxArgs a{};
     fill_common(p, a.c, bits, seed, sym0, n_sym, sym0 + n_sym);
     a.y = y;

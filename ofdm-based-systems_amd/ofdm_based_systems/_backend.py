@@ -162,7 +162,10 @@ def ptr(t: Optional[torch.Tensor]):
 
 
 def to_device(a: np.ndarray, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-    t = torch.from_numpy(np.ascontiguousarray(a))
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:  # e.g. np.frombuffer(bytes): torch wants a writable array
+        a = a.copy()
+    t = torch.from_numpy(a)
     if dtype is not None:
         t = t.to(dtype)
     return t.to(device(), non_blocking=False)
