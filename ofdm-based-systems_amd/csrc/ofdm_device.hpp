@@ -515,29 +515,38 @@ struct Slicer {
 };
 
 // Throughput-mode slicer (complex64, square QAM with b = FB <= 8 bits).  Both axes per
-// packed op: y = z * inv_step - lev0 * inv_step (the level coordinate, offset (side-1)/2
-// is a half-integer so it must be added before rounding), then y + 1.5*2^23 leaves
+// packed op: y = z * inv_step - lev0 * inv_step is the level coordinate (offset (side-1)/2,
+// a half-integer).  OFDM_SLICER_CLAMP (default): one v_pk_fma_f32 computes y / (side-1) of
+// both axes with the instruction's clamp bit, i.e. clamped to [0, 1] (every point beyond the
+// outer levels decides the outer level), and a second one v * (side-1) + 1.5*2^23 leaves
 // round(y) in the low mantissa bits (round-to-nearest-even; a tie is a decision boundary,
-// probability zero under noise), clamped to [0, side-1] on the raw bits by v_med3_i32.  The levels of
-// four elements are gathered into one selector word (byte j = element j) and looked up
+// probability zero under noise) -- two packed ops per element.  Otherwise y + 1.5*2^23
+// is clamped to [0, side-1] on the raw bits by two v_med3_i32 (four ops per element).  The levels
+// of four elements are gathered into one selector word (byte j = element j) and looked up
 // with v_perm_b32 in byte tables: four rx indices per instruction, byte-aligned like the
 // lane's tx bits (lane_bits).
+#ifndef OFDM_SLICER_CLAMP
+#define OFDM_SLICER_CLAMP 1
+#endif
 template <int FB>
 struct PermSlicer {
     static constexpr int SIDE = 1 << (FB / 2), HB = FB / 2;
     static constexpr int MAGIC = 0x4B400000;  // bit pattern of 1.5 * 2^23
     static constexpr uint32_t BYTE_MASK = 0x01010101u * ((1u << FB) - 1u);
-    f32x2 mul, add, magic;
+    f32x2 mul, add, magic, smax;
     uint32_t ti[4], tq[4];  // byte k: ipat[k] / qpat[k] << HB (k < SIDE)
 
     // scale: factor between the slicer input and the constellation's scale (1/sqrt(N)
     // when the FFT output is left unnormalised)
     __device__ void load(const AxisInfo& a, float scale) {
-        const float is = (float)(a.inv_step * (double)scale);
-        const float off = (float)(-a.lev0 * a.inv_step);
+        // clamp form: the level coordinate divided by side - 1 (QPSK: side - 1 = 1)
+        const double span = OFDM_SLICER_CLAMP ? (double)(SIDE - 1) : 1.0;
+        const float is = (float)(a.inv_step * (double)scale / span);
+        const float off = (float)(-a.lev0 * a.inv_step / span);
         mul = f32x2{is, is};
         add = f32x2{off, off};
         magic = f32x2{12582912.0f, 12582912.0f};
+        smax = f32x2{(float)(SIDE - 1), (float)(SIDE - 1)};
         for (int w = 0; w < 4; ++w) ti[w] = tq[w] = 0u;
         for (int k = 0; k < SIDE; ++k) {
             ti[k >> 2] |= (uint32_t)a.ipat[k] << (8 * (k & 3));
@@ -567,9 +576,21 @@ struct PermSlicer {
         uint32_t li[4], lq[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const f32x2 f = __builtin_elementwise_fma(z[j].v, mul, add) + magic;
-            li[j] = clampl(f.x);
-            lq[j] = clampl(f.y);
+            if constexpr (OFDM_SLICER_CLAMP) {
+                // both axes clamped to [0, 1] by the clamp bit of v_pk_fma_f32 (tools/clamp_probe.hip)
+                f32x2 v;
+                asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(v) : "v"(z[j].v), "v"(mul), "v"(add));
+                // the rounded levels taken as a 64-bit integer: read back as a float2 whose lanes
+                // are bit-cast, the compiler used lane 0 for both axes (as in adaptive_diff)
+                uint64_t fb;
+                asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(fb) : "v"(v), "v"(smax), "v"(magic));
+                li[j] = (uint32_t)fb;  // level in the low byte
+                lq[j] = (uint32_t)(fb >> 32);
+            } else {
+                const f32x2 f = __builtin_elementwise_fma(z[j].v, mul, add) + magic;
+                li[j] = clampl(f.x);
+                lq[j] = clampl(f.y);
+            }
         }
         const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
                                                   __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
