@@ -629,7 +629,8 @@ __device__ __forceinline__ uint32_t upat_lookup(uint32_t sel) {
 
 // Per-order slicer constants in LDS (one entry per LUT of the plan, entry 7 = unused
 // subcarrier): level coordinate y = z * mul + add, clamp bound MAGIC + side - 1, and
-// meta = tx bit mask (1 << b) - 1 | (1 << b/2) << 8.
+// meta = tx bit mask (1 << b) - 1 | (1 << b/2) << 8.  OFDM_SLICER_CLAMP: mul and add are
+// divided by side - 1 and smax holds side - 1 as a float (0 for the unused entry).
 struct OrderParams {
     float mul, add;
     uint32_t smax, meta;
@@ -643,6 +644,7 @@ template <bool SMALL>
 __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], const OrderParams* const (&op)[4],
                                                   uint32_t txw) {
     constexpr int MAGIC = 0x4B400000;  // bit pattern of 1.5 * 2^23: round(y) in the low mantissa
+    const f32x2 magic2 = f32x2{12582912.0f, 12582912.0f};
     uint32_t li[4], lq[4], meta[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -652,15 +654,29 @@ __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], cons
         // The result is taken as a 64-bit integer: read back as a float2 whose lanes are then
         // bit-cast, the compiler used lane 0 for both (reproduced in a 15-line kernel)
         const f32x2 ma = *(const f32x2*)&op[j]->mul;
-        uint64_t f;
-        asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
-            : "=v"(f)
-            : "v"(z[j].v), "v"(ma));
-        const float fx = __builtin_bit_cast(float, (uint32_t)f) + 12582912.0f;
-        const float fy = __builtin_bit_cast(float, (uint32_t)(f >> 32)) + 12582912.0f;
-        const int smax = (int)op[j]->smax;
-        li[j] = (uint32_t)min(max(__builtin_bit_cast(int, fx), MAGIC), smax);
-        lq[j] = (uint32_t)min(max(__builtin_bit_cast(int, fy), MAGIC), smax);
+        if constexpr (OFDM_SLICER_CLAMP) {
+            // clamp form (PermSlicer): (mul, add) hold the coordinate / (side - 1), clamped to
+            // [0, 1] by the clamp bit; smax holds side - 1 as a float, splatted by op_sel_hi
+            f32x2 v;
+            asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_hi:[0,1,0] clamp"
+                : "=v"(v)
+                : "v"(z[j].v), "v"(ma));
+            const f32x2 sm = *(const f32x2*)&op[j]->smax;
+            uint64_t f;
+            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(f) : "v"(v), "v"(sm), "v"(magic2));
+            li[j] = (uint32_t)f;
+            lq[j] = (uint32_t)(f >> 32);
+        } else {
+            uint64_t f;
+            asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
+                : "=v"(f)
+                : "v"(z[j].v), "v"(ma));
+            const float fx = __builtin_bit_cast(float, (uint32_t)f) + 12582912.0f;
+            const float fy = __builtin_bit_cast(float, (uint32_t)(f >> 32)) + 12582912.0f;
+            const int smax = (int)op[j]->smax;
+            li[j] = (uint32_t)min(max(__builtin_bit_cast(int, fx), MAGIC), smax);
+            lq[j] = (uint32_t)min(max(__builtin_bit_cast(int, fy), MAGIC), smax);
+        }
         // opaque to the v_perm byte-provider combine, which otherwise merges the Q gather
         // into the I gather (seen with run-time clamp bounds: the Q axis vanished)
         asm("" : "+v"(li[j]), "+v"(lq[j]));

@@ -687,12 +687,15 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     if constexpr (FB == 1) {
         if (threadIdx.x < 8) {
-            OrderParams o{0.f, 0.f, 0x4B400000u, 0u};  // unused subcarrier: level 0, no bits
+            // unused subcarrier: level 0, no bits
+            OrderParams o{0.f, 0.f, OFDM_SLICER_CLAMP ? 0u : 0x4B400000u, 0u};
             if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
                 const AxisInfo ax = cm.axis[threadIdx.x];
-                o.mul = (float)(ax.inv_step * cm.scale);  // the FFT output stays unscaled
-                o.add = (float)(-ax.lev0 * ax.inv_step);
-                o.smax = 0x4B400000u + (uint32_t)(ax.side - 1);
+                const double span = OFDM_SLICER_CLAMP ? (double)(ax.side - 1) : 1.0;  // see OrderParams
+                o.mul = (float)(ax.inv_step * cm.scale / span);  // the FFT output stays unscaled
+                o.add = (float)(-ax.lev0 * ax.inv_step / span);
+                o.smax = OFDM_SLICER_CLAMP ? __float_as_uint((float)(ax.side - 1))
+                                           : 0x4B400000u + (uint32_t)(ax.side - 1);
                 o.meta = ((1u << ax.bits) - 1u) | ((1u << ax.hbits) << 8);
             }
             ordt[threadIdx.x] = o;
