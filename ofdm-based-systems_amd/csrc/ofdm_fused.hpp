@@ -533,7 +533,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
                         const C ev = wb[w + (w >> 4)];
                         win[w] = f32x2{(float)ev.re, (float)ev.im};
                     }
-                    R pys = 0;
+                    f32x2 pacc = f32x2{0.f, 0.f};  // (sum Re^2, sum Im^2): one packed FMA per output
                     float4* yo = (float4*)(yout + sl * N + E * t);
 #pragma unroll
                     for (int j = 0; j < E; j += 2) {
@@ -546,9 +546,11 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
                             y1 = __builtin_elementwise_fma(e1.xx, hv[l], y1);
                             y1 = __builtin_elementwise_fma(e1.yy, hs[l], y1);
                         }
-                        pys += y0.x * y0.x + y0.y * y0.y + y1.x * y1.x + y1.y * y1.y;
+                        pacc = __builtin_elementwise_fma(y0, y0, pacc);
+                        pacc = __builtin_elementwise_fma(y1, y1, pacc);
                         if (yout && !(a.flags & 4)) yo[j >> 1] = float4{y0.x, y0.y, y1.x, y1.y};
                     }
+                    R pys = pacc.x + pacc.y;
                     if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
                         f32x2 yp = f32x2{0.f, 0.f};
 #pragma unroll
@@ -853,8 +855,15 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
         R nv = 0;
         if (eq == OFDM_EQ_MMSE) {
             R p = 0;
+            if constexpr (sizeof(R) == 4) {
+                f32x2 pacc = f32x2{0.f, 0.f};  // (sum Re^2, sum Im^2): one packed FMA per element
 #pragma unroll
-            for (int i = 0; i < E; ++i) p += norm2(x[i]);
+                for (int i = 0; i < E; ++i) pacc = __builtin_elementwise_fma(x[i].v, x[i].v, pacc);
+                p = pacc.x + pacc.y;
+            } else {
+#pragma unroll
+                for (int i = 0; i < E; ++i) p += norm2(x[i]);
+            }
             p = group_sum<R, TPS>(p, red);
             if constexpr (FB > 0) p *= scale * scale;  // power of the ortho-scaled spectrum
             nv = cm.gain_mean == 0.0 ? (R)INFINITY : ((p / (R)N) / (R)a.snr_lin) / (R)cm.gain_mean;
