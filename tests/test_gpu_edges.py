@@ -78,3 +78,27 @@ def test_ragged_offsets_tile_the_run(gpu, N, M, ch, eq, snr):
         eng.tx(eng.stream(), None, seed, a, b - a, parts[a:b], st)
     torch.cuda.synchronize()
     assert torch.equal(whole, parts)
+
+
+# the same launch-shape edges on the variant kernels: SC-OFDM + zero padding with 16-PSK sector
+# decisions (throughput FB = 4), 8-PSK (FB = 3), a prefix shorter than the channel, and adaptive
+# bit loading (FB = 1) -- through the case setup of the parity suite
+VARIANTS = [
+    (256, 16, "Lin-Phoong_P1", "MMSE", 14.0, {"scheme": "PSK", "modulator": "SC", "prefix": "ZP"}),
+    (1024, 8, "severe_multipath", "MMSE", 14.0, {"scheme": "PSK"}),
+    (256, 16, "severe_multipath", "MMSE", 12.0, {"cp": 2}),
+    (2048, 0, "Lin-Phoong_P1", "MMSE", 12.0, {"adaptive": True}),
+]
+
+
+@pytest.mark.parametrize("S", [1, 5, 11])
+@pytest.mark.parametrize("N,M,ch,eq,snr,var", VARIANTS, ids=[f"N{v[0]}-{'-'.join(map(str, v[5]))}" for v in VARIANTS])
+def test_ragged_variant_counts_match_oracle(gpu, N, M, ch, eq, snr, var, S):
+    from test_gpu_philox_parity import setup
+
+    eng, h, cp, kw = setup(N, M, ch, eq, B.OFDM_F32, var, snr)
+    res = eng.run(S, snr, seed=17)
+    ref = P.run_philox(17, S, N, M, h, cp, eq, snr, **kw)
+    for got, want in ((res.bit_errors, ref.bit_errors), (res.symbol_errors, ref.symbol_errors)):
+        assert abs(got - want) <= 3 + 1e-3 * want, (S, got, want)
+    assert res.power_sum == pytest.approx(ref.power_sum, rel=1e-5)
