@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define OFDM_ABI_VERSION 2
+#define OFDM_ABI_VERSION 3
 
 #define OFDM_OK 0
 #define OFDM_E_INVALID (-1)  /* bad argument / unsupported shape          */
@@ -83,6 +83,23 @@ typedef struct ofdm_desc {
     int32_t modulator;
 } ofdm_desc;
 
+/*
+ * Whole-stream statistics of the fused transmitter (ABI 3), one device record per run, zeroed
+ * by the caller and accumulated by every ofdm_tx of the run.  The AWGN power is the mean of |y|^2
+ * over the whole serial stream (noise/models.py:14); so that it -- and sigma -- does not depend on
+ * how a run is batched or sharded over GPUs, the sum is kept EXACTLY: every lane's share of one
+ * OFDM symbol is rounded once to 2^-40 fixed point and added as 32-bit limbs to 64-bit integers,
+ * power_fx[0] + 2^32 power_fx[1] (units of 2^-40).  Records of several ranks combine by adding
+ * the limbs (any order: integer arithmetic), then power_fx[1] += power_fx[0] >> 32,
+ * power_fx[0] &= 2^32 - 1, power_sum = power_fx[1] 2^-8 + power_fx[0] 2^-40 (IEEE double).
+ */
+typedef struct ofdm_stats {
+    double power_sum;     /* sum |y|^2 over all N+cp samples, = value of power_fx            */
+    double x_power_sum;   /* sum |x|^2 over the modulated samples incl. the guard          */
+    double x_peak;        /* max |x|^2 (simulation/models.py:519-522)                       */
+    int64_t power_fx[2];  /* sum |y|^2 in 2^-40 fixed point, 32-bit limbs (see above)       */
+} ofdm_stats;
+
 typedef struct ofdm_plan_info {
     int32_t n_fft, cp, precision, equalizer, n_taps;
     int32_t bits_per_ofdm_symbol; /* sum of bits over active subcarriers            */
@@ -125,6 +142,17 @@ int ofdm_map(ofdm_plan_t plan, void* stream, const uint8_t* bytes, int64_t n_byt
    packed MSB-first; fixed mode writes ceil(n*b/8) bytes (tail zero-padded), adaptive
    mode floor(S*sum(b)/8) bytes (constellation/adaptive.py:257-265). */
 int ofdm_demap(ofdm_plan_t plan, void* stream, const void* z, int64_t n, uint8_t* bytes);
+
+/* QAMConstellationMapper.decode (constellation/models.py:251-295) or
+   AdaptiveConstellationMapper.decode (constellation/adaptive.py:203-265) followed by
+   Simulation.run's error count (simulation/models.py:596-606), fused: Z is (n_sym, N)
+   equalised symbols in the plan precision, tx_bits the packed bits of those symbols (OFDM
+   symbol s from bit s*bits_per_ofdm_symbol, MSB first).  Nearest point per subcarrier as
+   ofdm_demap; counters[0] += bit errors (every bit in fixed mode, whole bytes of the run in
+   adaptive mode, as the reference's decode), counters[1] += symbol errors.  counters: 2 device
+   uint64 accumulated atomically. */
+int ofdm_demap_count(ofdm_plan_t plan, void* stream, const void* Z, const uint8_t* tx_bits,
+                     int64_t n_sym, uint64_t* counters);
 
 /* NNClassifier.classify (constellation/models.py:19-27) for an arbitrary LUT of M
    complex128 points: idx[i] = argmin_m |z_i - lut_m| (first on ties).  z is complex128. */
@@ -175,12 +203,12 @@ int ofdm_power(ofdm_plan_t plan, void* stream, const void* y, int64_t len, doubl
  *   the normalised CIR across symbol boundaries (channel/models.py:52-55).  Writes the
  *   channel-output samples of each symbol to y[(s-sym0)*ystride + n], ystride = N (the
  *   post-prefix samples) or N + cp with zero padding (all samples: the receiver
- *   overlap-adds the guard); y may be NULL (power pass only).  Accumulates into stats
- *   (device doubles): stats[0] += sum|y|^2 over all N+cp samples (noise/models.py:14),
- *   stats[1] += sum|x|^2, stats[2] = max(stats[2], max|x|^2) over the modulated samples
- *   incl. the guard (simulation/models.py:519-522).
+ *   overlap-adds the guard); y may be NULL (power pass only).  Accumulates into the device
+ *   record stats (ofdm_stats): sum|y|^2 over all N+cp samples (noise/models.py:14) in exact
+ *   fixed point, sum|x|^2 and max|x|^2 over the modulated samples incl. the guard
+ *   (simulation/models.py:519-522).
  *
- * ofdm_rx: adds AWGN with sigma^2 = (stats[0]/total_samples)/10^(snr/10) (noise_on=0:
+ * ofdm_rx: adds AWGN with sigma^2 = (stats->power_sum/total_samples)/10^(snr/10) (noise_on=0:
  *   no noise), strips the prefix (or overlap-adds the zero guard, prefix/models.py:69-101),
  *   FFT(ortho), equalises (MMSE noise variance per OFDM symbol, equalization/models.py:
  *   39-49), IFFT(ortho) for single carrier, decides the nearest constellation point
@@ -193,10 +221,10 @@ int ofdm_power(ofdm_plan_t plan, void* stream, const void* y, int64_t len, doubl
  *   call, (z_keep, N) complex -- the results' received_symbols (simulation/models.py:618).
  */
 int ofdm_tx(ofdm_plan_t plan, void* stream, const uint8_t* bits, uint64_t seed, int64_t sym0,
-            int64_t n_sym, void* y, double* stats);
+            int64_t n_sym, void* y, ofdm_stats* stats);
 
 int ofdm_rx(ofdm_plan_t plan, void* stream, const void* y, const double* nr, const double* ni,
-            uint64_t seed, const double* stats, int64_t total_samples, double snr_db,
+            uint64_t seed, const ofdm_stats* stats, int64_t total_samples, double snr_db,
             int32_t noise_on, const uint8_t* bits, int64_t sym0, int64_t n_sym,
             int64_t n_valid_bits, uint64_t* counters, void* z_out, int64_t z_keep);
 

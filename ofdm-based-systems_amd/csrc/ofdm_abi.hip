@@ -200,10 +200,16 @@ int psk_order(const double* lut, int m) {
     return m;
 }
 
-// Diagnostic ablation switches for timing studies (tools/ablate.py); unset = 0 = normal run.
+// Diagnostic ablation switches for timing studies (tools/ablate.py), read only by OFDM_ABLATION
+// builds; the product library runs every launch in full whatever the environment holds.
 int env_flags(const char* name) {
+#if OFDM_ABLATION
     const char* v = std::getenv(name);
     return v ? std::atoi(v) : 0;
+#else
+    (void)name;
+    return 0;
+#endif
 }
 
 int log2_exact(int n) {
@@ -566,6 +572,36 @@ int ofdm_demap(ofdm_plan_t p, void* stream, const void* z, int64_t n, uint8_t* b
     return OFDM_OK;
 }
 
+int ofdm_demap_count(ofdm_plan_t p, void* stream, const void* Z, const uint8_t* tx_bits, int64_t n_sym,
+                     uint64_t* counters) {
+    if (!p || !p->has_const) return fail(OFDM_E_INVALID, "plan has no constellation");
+    if (n_sym < 0 || (n_sym > 0 && (!Z || !tx_bits || !counters)))
+        return fail(OFDM_E_INVALID, "bad argument to ofdm_demap_count");
+    DemapCountArgs a{};
+    a.z = Z;
+    a.tx = tx_bits;
+    a.n_sym = n_sym;
+    const int64_t total = n_sym * (int64_t)p->bps;
+    // the reference compares every bit in FIXED mode, whole bytes in adaptive mode (its decode
+    // drops a trailing partial byte, constellation/adaptive.py:259-263)
+    a.n_valid_bits = p->adaptive ? (total / 8) * 8 : total;
+    a.n_tx_bytes = (total + 7) / 8;
+    a.n_fft = p->n;
+    a.b = p->b;
+    a.bps = p->bps;
+    a.adaptive = p->adaptive;
+    a.separable = p->separable;
+    a.sc = (const ScInfo*)p->sc.p;
+    a.axis = (const AxisInfo*)p->axis.p;
+    a.lut64 = (const double*)p->lut64.p;
+    a.lut_len = p->lut_len;
+    a.counters = (unsigned long long*)counters;
+#define CALL(R) launch_demap_count<R>(a, (hipStream_t)stream)
+    HIPCHK(DISPATCH(p, CALL));
+#undef CALL
+    return OFDM_OK;
+}
+
 int ofdm_nn_classify(void* stream, const double* lut, int32_t m, const void* z, int64_t n, int64_t* idx) {
     if (m < 1 || n < 0 || !lut || (n > 0 && (!z || !idx))) return fail(OFDM_E_INVALID, "bad argument to ofdm_nn_classify");
     HIPCHK(launch_nn_classify(lut, m, (const double*)z, n, idx, (hipStream_t)stream));
@@ -576,7 +612,7 @@ int ofdm_nn_classify(void* stream, const double* lut, int32_t m, const void* z, 
 static double* workspace(ofdm_plan_t p, void* stream) {
     std::lock_guard<std::mutex> lk(p->ws_mu);
     DevBuf& d = p->ws[stream];
-    if (!d.p && hipMalloc(&d.p, sizeof(double) * 3 * kMaxGrid) != hipSuccess) {
+    if (!d.p && hipMalloc(&d.p, sizeof(double) * kTxFields * kMaxGrid) != hipSuccess) {
         d.p = nullptr;
         return nullptr;
     }
@@ -666,7 +702,7 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
 }
 
 int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int64_t sym0, int64_t n_sym,
-            void* y, double* stats) {
+            void* y, ofdm_stats* stats) {
     if (!p || !p->has_const || p->L < 1) return fail(OFDM_E_INVALID, "ofdm_tx needs a constellation and channel taps");
     if (!p->separable && p->adaptive) return fail(OFDM_E_INVALID, "adaptive loading needs square-QAM constellations");
     if (p->L - 1 > p->n) return fail(OFDM_E_INVALID, "fused path needs channel order <= n_fft");
@@ -687,11 +723,12 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
 #define CALL(R) launch_tx<R>(p->logn, a, &grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));
 #undef CALL
-    return reduce_into(p, (hipStream_t)stream, a.partials, grid, 3, 4, stats);
+    HIPCHK(launch_finalize_tx(a.partials, grid, (double*)stats, (hipStream_t)stream));
+    return OFDM_OK;
 }
 
 int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const double* ni, uint64_t seed,
-            const double* stats, int64_t total_samples, double snr_db, int32_t noise_on, const uint8_t* bits,
+            const ofdm_stats* stats, int64_t total_samples, double snr_db, int32_t noise_on, const uint8_t* bits,
             int64_t sym0, int64_t n_sym, int64_t n_valid_bits, uint64_t* counters, void* z_out,
             int64_t z_keep) {
     if (!p || !p->has_const) return fail(OFDM_E_INVALID, "ofdm_rx needs a constellation");
@@ -706,7 +743,7 @@ int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const 
     a.y = y;
     a.nr = nr;
     a.ni = ni;
-    a.stats = stats;
+    a.stats = (const double*)stats;
     a.total_samples = total_samples;
     a.snr_lin = std::pow(10.0, snr_db / 10.0);
     a.noise_on = noise_on;

@@ -453,6 +453,102 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
     if constexpr (!LAST) sym_sync<G::TPS>();
 }
 
+// complex128 throughput kernels: the transposes between passes go through a row of N doubles,
+// real parts first, then imaginary parts -- half the LDS of a complex row per symbol, so twice
+// as many symbols (waves) fit a CU at the register budget complex128 needs.  Every pass takes
+// its inputs from x[] ("thread t owns elements t + i*TPS": element t + (q + r NB) TPS is input r
+// of butterfly q, which holds for every radix) and, unless LAST, leaves the next pass's inputs
+// there: its outputs go to the row at their Stockham positions, one component at a time, and
+// elements t + m*TPS come back.  With TPS <= 64 the exchange is wave-local (sym_sync = fences: a
+// wave's LDS operations execute in program order).
+template <typename R, int LOGN, int LOGR, int LOGNS, bool INV, bool LAST, bool TT>
+__device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb, const cpx<R>* lo,
+                                               const cpx<R>* hi, const cpx<R>* tt, int t) {
+    using G = Geo<LOGN>;
+    constexpr int RAD = 1 << LOGR;
+    constexpr int NS = 1 << LOGNS;
+    constexpr int NB = G::E / RAD;
+    cpx<R> v[NB][RAD];
+#pragma unroll
+    for (int q = 0; q < NB; ++q)
+#pragma unroll
+        for (int r = 0; r < RAD; ++r) v[q][r] = x[q + r * NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+        const int j = t + q * G::TPS;
+        const int k = j & (NS - 1);
+        if constexpr (LOGNS > 0 && TT) {
+            const cpx<R>* T = tt + (tt_size(LOGN) - tt_from(LOGN, LOGNS)) + k;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) v[q][r] = cmul(T[(r - 1) * NS], v[q][r]);
+        } else if constexpr (LOGNS > 0) {
+            const cpx<R> w1 = twiddle<R, LOGN, INV>(k << (LOGN - LOGNS - LOGR), lo, hi);
+            cpx<R> wr = w1;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) {
+                v[q][r] = cmul(wr, v[q][r]);
+                if (r + 1 < RAD) wr = cmul(wr, w1);
+            }
+        }
+        dft<R, RAD, INV>(v[q]);
+    }
+    if constexpr (LAST) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int r = 0; r < RAD; ++r) x[q + r * NB] = v[q][r];
+    } else {
+        auto put = [&](bool im) {
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                const int j = t + q * G::TPS;
+                const int idx = ((j >> LOGNS) << (LOGNS + LOGR)) + (j & (NS - 1));
+                if constexpr (NS % 16 == 0) {
+                    const int pi = pad(idx);
+                    static_for<0, RAD>([&](auto Rr) { rb[pad_plus<Rr * NS>(pi)] = im ? v[q][Rr].im : v[q][Rr].re; });
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RAD; ++r) rb[pad(idx + r * NS)] = im ? v[q][r].im : v[q][r].re;
+                }
+            }
+        };
+        auto get = [&](bool im) {
+            if constexpr (G::TPS % 16 == 0) {
+                const int pt = pad(t);
+                static_for<0, G::E>([&](auto M) {
+                    const R u = rb[pad_plus<M * G::TPS>(pt)];
+                    if (im) x[M].im = u; else x[M].re = u;
+                });
+            } else {
+#pragma unroll
+                for (int m = 0; m < G::E; ++m) {
+                    const R u = rb[pad(t + m * G::TPS)];
+                    if (im) x[m].im = u; else x[m].re = u;
+                }
+            }
+        };
+        put(false);
+        sym_sync<G::TPS>();
+        get(false);
+        sym_sync<G::TPS>();
+        put(true);
+        sym_sync<G::TPS>();
+        get(true);
+        sym_sync<G::TPS>();  // every read done before the next pass rewrites the row
+    }
+}
+
+template <typename R, int LOGN, int LOGNS, bool INV, bool TT>
+__device__ __forceinline__ void reg_passes_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb, const cpx<R>* lo,
+                                                 const cpx<R>* hi, const cpx<R>* tt, int t) {
+    if constexpr (LOGNS < LOGN) {
+        constexpr int REM = LOGN - LOGNS;
+        constexpr int LOGR = REM >= 4 ? 4 : REM;
+        reg_pass_split<R, LOGN, LOGR, LOGNS, INV, LOGNS + LOGR == LOGN, TT>(x, rb, lo, hi, tt, t);
+        reg_passes_split<R, LOGN, LOGNS + LOGR, INV, TT>(x, rb, lo, hi, tt, t);
+    }
+}
+
 template <typename R, int LOGN, int LOGNS, bool INV, bool TT>
 __device__ __forceinline__ void reg_passes(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, const cpx<R>* lo,
                                            const cpx<R>* hi, const cpx<R>* tt, int t) {
@@ -477,6 +573,22 @@ __device__ __forceinline__ void fft_reg(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf, 
         reg_passes<R, LOGN, 0, INV, TT>(x, buf, lo, hi, tt, t);
     }
 }
+
+// The same FFT with the split (real / imaginary) exchange; rb: the symbol's row of PADN reals.
+template <typename R, int LOGN, bool INV, bool TT>
+__device__ __forceinline__ void fft_reg_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb, const cpx<R>* lo,
+                                              const cpx<R>* hi, int t, const cpx<R>* tt) {
+    if constexpr (LOGN <= 4) {
+        dft<R, (1 << LOGN), INV>(x);
+    } else {
+        reg_passes_split<R, LOGN, 0, INV, TT>(x, rb, lo, hi, tt, t);
+    }
+}
+
+// Twiddle source of the throughput kernels: per-pass LDS tables (complex64 always; complex128
+// while the table fits beside the rows, N <= 1024: 16 KB) or the two-level table plus recurrence.
+template <typename R, int LOGN>
+constexpr bool fast_tt() { return sizeof(R) == 4 || LOGN <= 10; }
 
 // b (<= 8) bits at bit offset o of a stream stored as 32-bit words, stream bit 32w+j
 // = bit (31-j) of word w; one word of slack after the stream.
@@ -607,6 +719,51 @@ struct PermSlicer {
     }
 };
 
+// complex128 throughput slicer (same decisions and tables as PermSlicer): the level
+// coordinate of each axis is one v_fma_f64 with the clamp bit (y / (side - 1) clamped to
+// [0, 1]), and a second one v * (side - 1) + 1.5*2^52 leaves round(y) in the low mantissa word
+// (round-to-nearest-even; a tie is a decision boundary, probability zero under noise) -- both
+// in double precision, so a decision differs from the reference's float64 nearest-point search
+// only for points within ~1e-16 of a boundary.
+template <int FB>
+struct PermSlicer64 {
+    static constexpr int SIDE = 1 << (FB / 2), HB = FB / 2;
+    static constexpr uint32_t BYTE_MASK = 0x01010101u * ((1u << FB) - 1u);
+    double mul, add, smax;
+    uint32_t ti[4], tq[4];
+
+    __device__ void load(const AxisInfo& a, double scale) {
+        const double span = (double)(SIDE - 1);
+        mul = a.inv_step * scale / span;
+        add = -a.lev0 * a.inv_step / span;
+        smax = span;
+        for (int w = 0; w < 4; ++w) ti[w] = tq[w] = 0u;
+        for (int k = 0; k < SIDE; ++k) {
+            ti[k >> 2] |= (uint32_t)a.ipat[k] << (8 * (k & 3));
+            tq[k >> 2] |= ((uint32_t)a.qpat[k] << HB) << (8 * (k & 3));
+        }
+    }
+    __device__ __forceinline__ uint32_t level(double u) const {
+        double v;
+        asm("v_fma_f64 %0, %1, %2, %3 clamp" : "=v"(v) : "v"(u), "v"(mul), "v"(add));
+        const double f = __builtin_fma(v, smax, 6755399441055744.0);  // + 1.5 * 2^52
+        return (uint32_t)__builtin_bit_cast(uint64_t, f);
+    }
+    __device__ __forceinline__ uint32_t diff(const cpx<double> (&z)[4], uint32_t txw) const {
+        uint32_t li[4], lq[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            li[j] = level(z[j].re);
+            lq[j] = level(z[j].im);
+        }
+        const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
+                                                  __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
+        const uint32_t sq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(lq[3], lq[2], 0x0c0c0400u),
+                                                  __builtin_amdgcn_perm(lq[1], lq[0], 0x0c0c0400u), 0x05040100u);
+        return (PermSlicer<FB>::lookup(ti, si) | PermSlicer<FB>::lookup(tq, sq)) ^ (txw & BYTE_MASK);
+    }
+};
+
 // ------------------------------------------------------------------ adaptive throughput slicer
 // The reference's square-QAM LUTs (constellation/models.py:180-218) share one level -> index
 // pattern for every order: ipat_M[k] is the first sqrt(M) entries of
@@ -698,6 +855,29 @@ __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], cons
     const uint32_t mw = __builtin_amdgcn_perm(__builtin_amdgcn_perm(meta[3], meta[2], 0x0c0c0400u),
                                               __builtin_amdgcn_perm(meta[1], meta[0], 0x0c0c0400u), 0x05040100u);
     return (ib | qs) ^ (txw & mw);
+}
+
+// ------------------------------------------------------------------ exact power sums
+// The AWGN power is the whole-stream mean of |y|^2 (noise/models.py:14).  Summed in floating
+// point, its last bits would depend on how symbols are batched, sharded over GPUs and reduced, and
+// so would sigma.  Instead every lane's share of one OFDM symbol's sum |y|^2 -- a fixed set of
+// samples, summed in a fixed order -- is rounded once to 2^-40 fixed point and accumulated as two
+// 32-bit limbs in 64-bit integers: the total is exact integer arithmetic, independent of every
+// grouping.  Value = limb1 2^-8 + limb0 2^-40 (kFxLo / kFxHi), limb0 < 2^32 after normalisation;
+// a lane's share is < 2^24 (unit-power signals), so limb1 stays exact in a double.
+constexpr double kFxHi = 0x1p-8, kFxLo = 0x1p-40;
+__device__ __forceinline__ void fx_accum(double p, unsigned long long& l0, unsigned long long& l1) {
+    const double a = p * 256.0;  // exact
+    const double hi = floor(a);
+    l1 += (unsigned long long)(uint32_t)hi;
+    l0 += (unsigned long long)(uint32_t)rint((a - hi) * 4294967296.0);  // (a - hi) exact; <= 2^32
+}
+__host__ __device__ inline void fx_normalize(unsigned long long& l0, unsigned long long& l1) {
+    l1 += l0 >> 32;
+    l0 &= 0xFFFFFFFFull;
+}
+__host__ __device__ inline double fx_value(unsigned long long l0, unsigned long long l1) {
+    return (double)l1 * kFxHi + (double)l0 * kFxLo;
 }
 
 // ------------------------------------------------------------------ reductions

@@ -65,11 +65,19 @@
 
 namespace ofdm {
 
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+
 template <bool NT, typename C>
 __device__ __forceinline__ C ld_stream(const C* p) {
     if constexpr (NT && sizeof(C) == 8) {
         C v;
         v.v = __builtin_nontemporal_load((const f32x2*)p);
+        return v;
+    } else if constexpr (NT && sizeof(C) == 16) {
+        const f64x2 u = __builtin_nontemporal_load((const f64x2*)p);
+        C v;
+        v.re = u.x;
+        v.im = u.y;
         return v;
     } else {
         return *p;
@@ -89,6 +97,15 @@ __device__ __forceinline__ void st_stream(__attribute__((address_space(1))) cpx<
         __builtin_nontemporal_store(v.v, (gf2*)p);
     else
         *(gf2*)p = v.v;
+}
+template <bool NT>
+__device__ __forceinline__ void st_stream(__attribute__((address_space(1))) cpx<double>* p, cpx<double> v) {
+    typedef __attribute__((address_space(1))) f64x2 gd2;
+    const f64x2 u = f64x2{v.re, v.im};
+    if constexpr (NT)
+        __builtin_nontemporal_store(u, (gd2*)p);
+    else
+        *(gd2*)p = u;
 }
 
 // Global-memory (address space 1) pointers: a pointer rebuilt from an integer would
@@ -115,11 +132,40 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 #ifndef OFDM_TX_MP_BLOCK
 #define OFDM_TX_MP_BLOCK 256
 #endif
+// complex128 throughput kernels (R = double, FB > 0).  The FFT exchanges through split real /
+// imaginary rows (fft_reg_split: 8.5 KB per N = 1024 symbol), so the occupancy is set by the
+// registers: 16 complex128 elements per lane plus a radix-16 butterfly -- RX ~160 VGPRs (3 waves
+// per SIMD: one 768-thread workgroup of 12 symbols per CU), flat TX 128 (4 waves: 1024 threads).
+// The FIR TX keeps complex rows (the FIR window reads the extended stream): 512 threads at
+// 2 waves per SIMD, 256 below N = 1024 where 512 threads' rows exceed the LDS.
+#ifndef OFDM_F64_TX_BLOCK
+#define OFDM_F64_TX_BLOCK 1024
+#endif
+#ifndef OFDM_F64_TX_WAVES
+#define OFDM_F64_TX_WAVES 4
+#endif
+#ifndef OFDM_F64_RX_BLOCK
+#define OFDM_F64_RX_BLOCK 768
+#endif
+#ifndef OFDM_F64_RX_WAVES
+#define OFDM_F64_RX_WAVES 3
+#endif
+#ifndef OFDM_F64_FIR_BLOCK
+#define OFDM_F64_FIR_BLOCK 512
+#endif
 // LT (throughput TX): 0 flat channel; 4 / 8 multipath with <= LT taps through the register
 // window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps)
-template <int FB, int LOGN, int LT>
+template <typename R, int FB, int LOGN, int LT>
 constexpr int tx_block() {
+    if (sizeof(R) == 8 && FB > 0)
+        return LT == 0 ? OFDM_F64_TX_BLOCK : (LOGN < 10 ? 256 : OFDM_F64_FIR_BLOCK);
     return FB > 0 && LOGN <= 10 ? (LT != 0 ? OFDM_TX_MP_BLOCK : OFDM_TX_FAST_BLOCK) : kBlock;
+}
+constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
+template <typename R, int FB, int LOGN, int LT>
+constexpr int tx_waves() {
+    if (sizeof(R) == 8 && FB > 0) return LT == 0 ? OFDM_F64_TX_WAVES : 2;
+    return block_waves(tx_block<R, FB, LOGN, LT>(), FB > 0 && LT > 0 ? OFDM_TX_WFIR_WAVES : OFDM_TX_WAVES);
 }
 // padded FIR row index of the throughput multipath TX: one slot per 16 elements
 __host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
@@ -136,18 +182,19 @@ __host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
 #ifndef OFDM_RX_PF_WAVES
 #define OFDM_RX_PF_WAVES 3
 #endif
-template <int FB, int LOGN>
-constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && FB > 1 && LOGN >= 6 && LOGN <= 10; }
-template <int FB, int LOGN, int EQ>
+template <typename R, int FB, int LOGN>
+constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB > 1 && LOGN >= 6 && LOGN <= 10; }
+template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_block() {
-    return rx_prefetch<FB, LOGN>() ? kBlock
-                                    : (FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock);
+    if (sizeof(R) == 8 && FB > 0) return LOGN <= 10 ? OFDM_F64_RX_BLOCK : 512;
+    return rx_prefetch<R, FB, LOGN>() ? kBlock
+                                       : (FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock);
 }
-template <int FB, int LOGN, int EQ>
+template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_waves() {
-    return rx_prefetch<FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
+    if (sizeof(R) == 8 && FB > 0) return LOGN <= 10 ? OFDM_F64_RX_WAVES : 2;
+    return rx_prefetch<R, FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
 }
-constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 // throughput RX: equaliser coefficients staged in LDS up to N = 2^OFDM_EQ_LDS_MAX_LOGN (beyond,
 // the table would cost a resident workgroup per CU)
 #ifndef OFDM_EQ_LDS_MAX_LOGN
@@ -158,6 +205,9 @@ constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 #endif
 template <int FB, int LOGN, int EQ>
 constexpr bool eq_in_lds() { return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= OFDM_EQ_LDS_MAX_LOGN; }
+// complex128 throughput kernels exchange FFT data through rows of reals (fft_reg_split)
+template <typename R, int FB>
+constexpr bool split_rows() { return sizeof(R) == 8 && FB > 0; }
 
 // Reference mode: stage OFDM symbol s's tx bits from the packed bytes of the run
 // (symbol s starts at bit s*bps, zeros past the end) as 32-bit words in W
@@ -180,10 +230,14 @@ __device__ __forceinline__ int stage_words(const TxRxCommon& a, int64_t s, uint3
 
 template <typename R>
 __device__ __forceinline__ R recip(R d) {
-    if constexpr (sizeof(R) == 4)
+    if constexpr (sizeof(R) == 4) {
         return __builtin_amdgcn_rcpf(d);  // v_rcp_f32 (1 ulp): throughput mode
-    else
-        return (R)1 / d;
+    } else {
+        // v_rcp_f64 and two Newton steps (~1 ulp) instead of the IEEE division sequence
+        R r = __builtin_amdgcn_rcp(d);
+        r = __builtin_fma(__builtin_fma(-d, r, (R)1), r, r);
+        return __builtin_fma(__builtin_fma(-d, r, (R)1), r, r);
+    }
 }
 
 // MMSE filter coefficient conj(H)/(|H|^2 + nv) (equalization/models.py:58-61).  In f64 the
@@ -250,17 +304,18 @@ struct TxBits {
 // three reflections are undone on the sector index k; the LUT index is gray(k).  M = 2 and
 // 4 have no in-octant boundaries.  Decisions differ from the brute-force search only on a
 // decision boundary (|y| = |x| or an exact tangent), a probability-zero event under noise.
-__device__ __forceinline__ uint32_t psk_decide(cpx<float> v, const TxRxCommon& cm) {
+template <typename R>
+__device__ __forceinline__ uint32_t psk_decide(cpx<R> v, const TxRxCommon& cm) {
     const int M = cm.psk_m;
-    const float ax = fabsf(v.re), ay = fabsf(v.im);
-    const bool sw = ay > ax, sx = v.re < 0.f, sy = v.im < 0.f;
-    const float u = fmaxf(ax, ay), w = fminf(ax, ay);  // angle of (u, w) in [0, pi/4]
+    const R ax = fabs(v.re), ay = fabs(v.im);
+    const bool sw = ay > ax, sx = v.re < (R)0, sy = v.im < (R)0;
+    const R u = fmax(ax, ay), w = fmin(ax, ay);  // angle of (u, w) in [0, pi/4]
     int k;
     if (M == 2) {
         k = sx ? 1 : 0;
     } else {
         int q = 0;
-        for (int j = 0; j < (M >> 3); ++j) q += w > cm.psk_tan[j] * u;
+        for (int j = 0; j < (M >> 3); ++j) q += w > (R)cm.psk_tan[j] * u;
         const int quarter = M >> 2;
         int k1 = sw ? quarter - q : q;        // reflect about 45 degrees
         if (M == 4) k1 = sw ? 1 : 0;
@@ -296,21 +351,35 @@ __device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm) {
 }
 
 
+// FFT of one symbol in a fused kernel: complex128 throughput kernels exchange through a row of
+// reals (fft_reg_split), complex64 ones through the complex row with per-pass LDS twiddles, the
+// generic kernel with the two-level table and recurrence.
+template <typename R, int LOGN, bool INV, int FB>
+__device__ __forceinline__ void fft_sym(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* row, const cpx<R>* tw,
+                                        const cpx<R>* tt, int t) {
+    if constexpr (split_rows<R, FB>())
+        fft_reg_split<R, LOGN, INV, fast_tt<R, LOGN>()>(x, (R*)row, tw, tw + 64, t, tt);
+    else
+        fft_reg<R, LOGN, INV, (FB > 0)>(x, row, tw, tw + 64, t, tt);
+}
+// per-pass twiddle tables in LDS (throughput kernels while they fit) vs the two-level table
+template <typename R, int LOGN, int FB>
+constexpr bool uses_tt() { return FB > 0 && fast_tt<R, LOGN>(); }
+
 // ============================================================ fused TX
 // Each symbol group walks `chunk` consecutive OFDM symbols so the FIR tail (last L-1
 // stream samples of the previous symbol) is carried in LDS; the first symbol of a chunk
 // regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
 template <typename R, int LOGN, int FB, int LT>
-__global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
-                             (block_waves(tx_block<FB, LOGN, LT>(),
-                                          FB > 0 && LT > 0 ? OFDM_TX_WFIR_WAVES : OFDM_TX_WAVES))) void k_tx(
+__global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOGN, LT>())) void k_tx(
     TxArgs a) {
-    constexpr int BLK = tx_block<FB, LOGN, LT>();
+    constexpr int BLK = tx_block<R, FB, LOGN, LT>();
     constexpr bool WFIR = FB > 0 && LT > 0;  // register window FIR
     using G = Geo<LOGN, BLK>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
     const TxRxCommon& cm = a.c;
+    const int flags = ablation_flags(a.flags);
     const bool adaptive = FB ? false : (bool)cm.adaptive;
     // generic kernel variants: single-carrier OFDM (no IFFT, modulation/models.py:
     // 58-70) and the zero-padding guard (prefix/models.py:55-67: [x | 0 ... 0])
@@ -324,8 +393,11 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
     const int cp = cm.cp, L = LT != 0 ? a.L : 1;
     const int slot = a.slot;  // complex elements per symbol row (>= PADN and >= L-1+cp+N)
     const int tls = L > 1 ? L - 1 : 1;
+    constexpr bool TT = uses_tt<R, LOGN, FB>();
+    // complex128 flat TX: the row only carries the FFT exchange, a row of reals (fft_reg_split)
+    constexpr bool ROW_REAL = split_rows<R, FB>() && LT == 0;
     Carve cv(ofdm_smem);
-    C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
+    C* tw = cv.take<C>(TT ? 0 : 128);  // two-level twiddles (generic kernel, complex128 N > 1024)
     // throughput kernels: the LUT in static LDS at a link-time address, so an element's LUT read
     // is addressed by its index bits alone (2^FB entries; adaptive: the pool + a zero entry);
     // generic kernel: dynamic
@@ -335,17 +407,17 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
     C* h = cv.take<C>(32);
     C* hsw = cv.take<C>(WFIR ? 32 : 0);  // window FIR: the taps swizzled, (-im, re)
     AxisInfo* axis = cv.take<AxisInfo>(4);
-    C* rows = cv.take<C>((size_t)G::SPB * slot);
+    unsigned char* rowmem = cv.take<unsigned char>((size_t)G::SPB * slot * (ROW_REAL ? sizeof(R) : sizeof(C)));
     C* tails = cv.take<C>((size_t)G::SPB * tls);
     uint32_t* words = cv.take<uint32_t>(FB ? 0 : (size_t)G::SPB * cm.words_per_sym);  // reference bits
     double* red = cv.take<double>(BLK / 64);
-    constexpr int TTS = FB ? tt_size(LOGN) : 0;
+    constexpr int TTS = TT ? tt_size(LOGN) : 0;
     C* tt = cv.take<C>(TTS);  // throughput kernel: inverse per-pass twiddles
     // adaptive throughput kernel: per subcarrier (LUT offset << 8 | tx bit mask); unused
     // subcarriers point at a zero entry appended to the LUT pool
     uint32_t* sce = cv.take<uint32_t>(FB == 1 ? N : 0);
 
-    if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
+    if constexpr (!TT) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
     // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element);
     // flat throughput kernel: the channel tap too (y = h0 ifft(X) = ifft(h0 X)), so the
@@ -373,7 +445,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
 
     const int ls = TPS >= 64 ? __builtin_amdgcn_readfirstlane(threadIdx.x / TPS) : threadIdx.x / TPS;
     const int t = threadIdx.x % TPS;
-    C* row = rows + ls * slot;
+    C* row = (C*)(rowmem + (size_t)ls * slot * (ROW_REAL ? sizeof(R) : sizeof(C)));
     C* tl = tails + ls * tls;
     uint32_t* W = words + ls * cm.words_per_sym;
     C* yout = (C*)a.y;
@@ -385,7 +457,9 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
     const int A = (cp + 15) & ~15, R0 = A - cp + LTN - 1;
     const int64_t ngroups = (cm.n_sym + a.chunk - 1) / a.chunk;
     const int64_t niter = (ngroups + G::SPB - 1) / G::SPB;
-    double py = 0, px = 0, mx = 0;
+    // sum |y|^2 in exact fixed point (fx_accum, per lane and symbol); |x|^2 statistics in double
+    unsigned long long pq0 = 0, pq1 = 0;
+    double px = 0, mx = 0;
 
     for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
         const int64_t grp = it * G::SPB + ls;
@@ -395,7 +469,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
             const int64_t sg = cm.sym0 + sl;
             const bool active = grp < ngroups && sl < cm.n_sym && sg >= 0;
             TxBits<FB, TPS> tb;
-            tb.load(cm, sg, t, W, active && !(a.flags & 1));
+            tb.load(cm, sg, t, W, active && !(flags & 1));
             if (FB == 0) sym_sync<TPS>();  // staged words visible
             // map (QAMConstellationMapper.encode, constellation/models.py:240-246); the
             // 1/sqrt(N) of ifft(norm="ortho") folded in
@@ -431,7 +505,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
                     x[i] = v;
                 }
             }
-            if (!(a.flags & 2) && !scm) fft_reg<R, LOGN, true, (FB > 0)>(x, row, tw, tw + 64, t, tt);
+            if (!(flags & 2) && !scm) fft_sym<R, LOGN, true, FB>(x, row, tw, tt, t);
             // The prefix repeats samples k >= N - cp.  With cp <= TPS only the lane's last
             // element can be one of them (one loop-invariant compare); otherwise the compares
             // are made per symbol against an opaque copy of N - cp, so they are not hoisted
@@ -468,7 +542,7 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
 #pragma unroll
                     for (int i = 0; i < E; ++i) {
                         const C yv = FOLD_H0 ? x[i] : cmul(h0, x[i]);
-                        if (!yout || (a.flags & 4)) continue;
+                        if (!yout || (flags & 4)) continue;
                         if constexpr (FB > 0 && TPS >= 64) {
                             // the row base is wave-uniform: made explicit, the stores take the
                             // SGPR-base + 32-bit lane-offset form instead of a loop-carried 64-bit
@@ -482,15 +556,15 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
                     if (zp && yout)
                         for (int j = t; j < cp; j += TPS) yo[N + j] = mk<R>(0, 0);
                     if constexpr (FOLD_H0) {
-                        py += pxs;  // the statistics above were taken on y (x |h0|^2 fixed below)
+                        fx_accum((double)pxs, pq0, pq1);  // the statistics above were taken on y (x |h0|^2 fixed below)
                     } else if constexpr (FB > 0) {
-                        py += (double)(norm2(h0) * pxs);  // |y|^2 = |h0|^2 |x|^2 (complex64 mode)
+                        fx_accum((double)(norm2(h0) * pxs), pq0, pq1);  // |y|^2 = |h0|^2 |x|^2 (complex64 mode)
                     } else {
                         R pys = 0;
 #pragma unroll
                         for (int i = 0; i < E; ++i) pys += norm2(cmul(h0, x[i]));
                         pys += prefix_sum([&](int i) { return norm2(cmul(h0, x[i])); });
-                        py += pys;
+                        fx_accum((double)pys, pq0, pq1);
                     }
                 }
                 sym_sync<TPS>();  // W / row reuse by the next symbol
@@ -514,55 +588,88 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
                     row[fir_pad(R0 - (LT - 1) + t)] = z < 0 ? mk<R>(0, 0) : tl[z];
                 }
                 sym_sync<TPS>();
-                if (active && c >= 0) {
-                    // taps (zero past L), LDS broadcast reads; the opaque offset keeps the reads
-                    // in the symbol loop (hoisted, the 4 LT registers stay live through the FFT
-                    // and spill)
-                    int ho = 0;
-                    asm volatile("" : "+v"(ho));
-                    f32x2 hv[LT], hs[LT];
+                if constexpr (sizeof(R) == 8) {
+                    if (active && c >= 0) {
+                        // complex128: the same register window, one complex FMA chain per output
+                        // (4 v_fma_f64 per tap)
+                        int ho = 0;
+                        asm volatile("" : "+v"(ho));
+                        C hq[LT];
 #pragma unroll
-                    for (int q = 0; q < LT; ++q) {
-                        hv[q] = f32x2{(float)h[ho + q].re, (float)h[ho + q].im};
-                        hs[q] = f32x2{(float)hsw[ho + q].re, (float)hsw[ho + q].im};
-                    }
-                    const C* wb = row + (A + (A >> 4) + 17 * t);
-                    f32x2 win[WN];
+                        for (int q = 0; q < LT; ++q) hq[q] = h[ho + q];
+                        const C* wb = row + (A + (A >> 4) + 17 * t);
+                        C win[WN];
 #pragma unroll
-                    for (int w = 0; w < WN; ++w) {
-                        const C ev = wb[w + (w >> 4)];
-                        win[w] = f32x2{(float)ev.re, (float)ev.im};
-                    }
-                    f32x2 pacc = f32x2{0.f, 0.f};  // (sum Re^2, sum Im^2): one packed FMA per output
-                    float4* yo = (float4*)(yout + sl * N + E * t);
+                        for (int w = 0; w < WN; ++w) win[w] = wb[w + (w >> 4)];
+                        R pys = 0;
+                        C* yo = yout + sl * N + E * t;
 #pragma unroll
-                    for (int j = 0; j < E; j += 2) {
-                        f32x2 y0 = f32x2{0.f, 0.f}, y1 = f32x2{0.f, 0.f};
+                        for (int j = 0; j < E; ++j) {
+                            C yv = mk<R>(0, 0);
 #pragma unroll
-                        for (int l = 0; l < LT; ++l) {
-                            const f32x2 e0 = win[j + LT - 1 - l], e1 = win[j + LT - l];
-                            y0 = __builtin_elementwise_fma(e0.xx, hv[l], y0);
-                            y0 = __builtin_elementwise_fma(e0.yy, hs[l], y0);
-                            y1 = __builtin_elementwise_fma(e1.xx, hv[l], y1);
-                            y1 = __builtin_elementwise_fma(e1.yy, hs[l], y1);
+                            for (int l = 0; l < LT; ++l) yv = yv + cmul(hq[l], win[j + LT - 1 - l]);
+                            pys += norm2(yv);
+                            if (yout && !(flags & 4)) yo[j] = yv;
                         }
-                        pacc = __builtin_elementwise_fma(y0, y0, pacc);
-                        pacc = __builtin_elementwise_fma(y1, y1, pacc);
-                        if (yout && !(a.flags & 4)) yo[j >> 1] = float4{y0.x, y0.y, y1.x, y1.y};
-                    }
-                    R pys = pacc.x + pacc.y;
-                    if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
-                        f32x2 yp = f32x2{0.f, 0.f};
+                        if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
+                            C yp = mk<R>(0, 0);
 #pragma unroll
-                        for (int l = 0; l < LT; ++l) {
-                            const C ev = row[fir_pad(R0 + t - l)];
-                            const f32x2 e = f32x2{(float)ev.re, (float)ev.im};
-                            yp = __builtin_elementwise_fma(e.xx, hv[l], yp);
-                            yp = __builtin_elementwise_fma(e.yy, hs[l], yp);
+                            for (int l = 0; l < LT; ++l) yp = yp + cmul(hq[l], row[fir_pad(R0 + t - l)]);
+                            pys += norm2(yp);
                         }
-                        pys += yp.x * yp.x + yp.y * yp.y;
+                        fx_accum((double)pys, pq0, pq1);
                     }
-                    py += pys;
+                } else {
+                    if (sizeof(R) == 4 && active && c >= 0) {
+                        // taps (zero past L), LDS broadcast reads; the opaque offset keeps the reads
+                        // in the symbol loop (hoisted, the 4 LT registers stay live through the FFT
+                        // and spill)
+                        int ho = 0;
+                        asm volatile("" : "+v"(ho));
+                        f32x2 hv[LT], hs[LT];
+#pragma unroll
+                        for (int q = 0; q < LT; ++q) {
+                            hv[q] = f32x2{(float)h[ho + q].re, (float)h[ho + q].im};
+                            hs[q] = f32x2{(float)hsw[ho + q].re, (float)hsw[ho + q].im};
+                        }
+                        const C* wb = row + (A + (A >> 4) + 17 * t);
+                        f32x2 win[WN];
+#pragma unroll
+                        for (int w = 0; w < WN; ++w) {
+                            const C ev = wb[w + (w >> 4)];
+                            win[w] = f32x2{(float)ev.re, (float)ev.im};
+                        }
+                        f32x2 pacc = f32x2{0.f, 0.f};  // (sum Re^2, sum Im^2): one packed FMA per output
+                        float4* yo = (float4*)(yout + sl * N + E * t);
+#pragma unroll
+                        for (int j = 0; j < E; j += 2) {
+                            f32x2 y0 = f32x2{0.f, 0.f}, y1 = f32x2{0.f, 0.f};
+#pragma unroll
+                            for (int l = 0; l < LT; ++l) {
+                                const f32x2 e0 = win[j + LT - 1 - l], e1 = win[j + LT - l];
+                                y0 = __builtin_elementwise_fma(e0.xx, hv[l], y0);
+                                y0 = __builtin_elementwise_fma(e0.yy, hs[l], y0);
+                                y1 = __builtin_elementwise_fma(e1.xx, hv[l], y1);
+                                y1 = __builtin_elementwise_fma(e1.yy, hs[l], y1);
+                            }
+                            pacc = __builtin_elementwise_fma(y0, y0, pacc);
+                            pacc = __builtin_elementwise_fma(y1, y1, pacc);
+                            if (yout && !(flags & 4)) yo[j >> 1] = float4{y0.x, y0.y, y1.x, y1.y};
+                        }
+                        R pys = pacc.x + pacc.y;
+                        if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
+                            f32x2 yp = f32x2{0.f, 0.f};
+#pragma unroll
+                            for (int l = 0; l < LT; ++l) {
+                                const C ev = row[fir_pad(R0 + t - l)];
+                                const f32x2 e = f32x2{(float)ev.re, (float)ev.im};
+                                yp = __builtin_elementwise_fma(e.xx, hv[l], yp);
+                                yp = __builtin_elementwise_fma(e.yy, hs[l], yp);
+                            }
+                            pys += yp.x * yp.x + yp.y * yp.y;
+                        }
+                        fx_accum((double)pys, pq0, pq1);
+                    }
                 }
                 // tail for the next symbol: the last L-1 stream samples (zeros before symbol 0)
                 if (t < L - 1) tl[t] = active ? row[fir_pad(R0 + N + cp - (L - 1) + t)] : mk<R>(0, 0);
@@ -596,14 +703,14 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
 #pragma unroll 8
                         for (int l = 0; l < L; ++l) yv = yv + cmul(h[l], e[-l]);
                         pys += norm2(yv);
-                        if (yout && !(a.flags & 4)) {
+                        if (yout && !(flags & 4)) {
                             if (zp)
                                 yout[sl * ystride + m] = yv;  // every stream sample (RX overlap-adds)
                             else if (m >= cp)
                                 yout[sl * N + (m - cp)] = yv;
                         }
                     }
-                    py += pys;
+                    fx_accum((double)pys, pq0, pq1);
                 }
                 // tail for the next symbol: the last L-1 stream samples (zeros before symbol 0)
                 for (int j = t; j < L - 1; j += TPS) tl[j] = active ? row[N + cp + j] : mk<R>(0, 0);
@@ -616,26 +723,31 @@ __global__ __launch_bounds__((tx_block<FB, LOGN, LT>()),
         px *= ih2;
         mx *= ih2;
     }
-    py = block_sum<double, BLK>(py, red);
+    fx_normalize(pq0, pq1);
+    pq0 = block_sum<unsigned long long, BLK>(pq0, (unsigned long long*)red);
+    pq1 = block_sum<unsigned long long, BLK>(pq1, (unsigned long long*)red);
     px = block_sum<double, BLK>(px, red);
     mx = block_max<double, BLK>(mx, red);
     if (threadIdx.x == 0) {
-        a.partials[blockIdx.x * 3 + 0] = py;
-        a.partials[blockIdx.x * 3 + 1] = px;
-        a.partials[blockIdx.x * 3 + 2] = mx;
+        unsigned long long* pr = (unsigned long long*)a.partials + (size_t)blockIdx.x * kTxFields;
+        pr[0] = pq0;
+        pr[1] = pq1;
+        a.partials[(size_t)blockIdx.x * kTxFields + 2] = px;
+        a.partials[(size_t)blockIdx.x * kTxFields + 3] = mx;
     }
 }
 
 // ============================================================ fused RX
 // EQ: OFDM_EQ_* fixed at compile time (throughput kernel) or -1 = from the plan.
 template <typename R, int LOGN, int EQ, int FB>
-__global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>())) void k_rx(
+__global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOGN, EQ>())) void k_rx(
     RxArgs a) {
-    constexpr int BLK = rx_block<FB, LOGN, EQ>();
+    constexpr int BLK = rx_block<R, FB, LOGN, EQ>();
     using G = Geo<LOGN, BLK>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
     const TxRxCommon& cm = a.c;
+    const int flags = ablation_flags(a.flags);
     const int eq = EQ >= 0 ? EQ : cm.eq;
     const bool adaptive = FB ? false : (bool)cm.adaptive;
     // generic kernel variants: single-carrier OFDM (FFT -> equalise -> IFFT,
@@ -651,13 +763,15 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     // (its byte offset) address an entry with no add
     __shared__ f32x2 ntab[kNoisePhases];
     Carve cv(ofdm_smem);
-    C* tw = cv.take<C>(FB ? 0 : 128);  // two-level twiddles (generic kernel)
+    constexpr bool TT = uses_tt<R, LOGN, FB>();
+    constexpr bool SPLIT = split_rows<R, FB>();  // complex128 throughput: rows of reals
+    C* tw = cv.take<C>(TT ? 0 : 128);  // two-level twiddles (generic kernel, complex128 N > 1024)
     AxisInfo* axis = cv.take<AxisInfo>(4);
-    C* rows = cv.take<C>((size_t)G::SPB * G::PADN);
+    unsigned char* rowmem = cv.take<unsigned char>((size_t)G::SPB * G::PADN * (SPLIT ? sizeof(R) : sizeof(C)));
     uint32_t* words = cv.take<uint32_t>(FB ? 0 : (size_t)G::SPB * cm.words_per_sym);  // reference bits
     R* red = cv.take<R>(BLK / 64);
     unsigned long long* redc = cv.take<unsigned long long>(BLK / 64);
-    constexpr int TTS = FB ? tt_size(LOGN) : 0;
+    constexpr int TTS = TT ? tt_size(LOGN) : 0;
     // throughput kernel: forward per-pass twiddles, plus the inverse ones for SC-OFDM's IFFT
     const int tts_all = FB > 1 && scm ? 2 * TTS : TTS;
     C* tt = cv.take<C>(tts_all);
@@ -674,7 +788,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
         OFDM_EQ_PRE && !EQ_LDS && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
-    const bool noise = a.noise_on && !(a.flags & 1);
+    const bool noise = a.noise_on && !(flags & 1);
     double sigma_d = 0;
     if (noise) {
         const double p = a.stats[0] / (double)a.total_samples;
@@ -682,7 +796,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     }
     const R sigma = (R)sigma_d;
     build_noise_table(ntab, sigma_d);
-    if constexpr (FB == 0) load_twiddles<R>(tw, (const C*)cm.tw);
+    if constexpr (!TT) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
     if constexpr (EQ_LDS)
         for (int k = threadIdx.x; k < N; k += BLK) eqt[k] = ((const C*)cm.eq_a)[k];
@@ -708,7 +822,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     // a symbol group of >= 64 threads is whole wavefronts: make its index wave-uniform
     const int ls = TPS >= 64 ? __builtin_amdgcn_readfirstlane(threadIdx.x / TPS) : threadIdx.x / TPS;
     const int t = threadIdx.x % TPS;
-    C* row = rows + ls * G::PADN;
+    C* row = (C*)(rowmem + (size_t)ls * G::PADN * (SPLIT ? sizeof(R) : sizeof(C)));
     uint32_t* W = words + ls * cm.words_per_sym;
     const C* eqa = (const C*)cm.eq_a;
     const R* eqb = (const R*)cm.eq_b;
@@ -730,7 +844,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     const int cp = cm.cp;
     const R scale = (R)cm.scale;
     Slicer<R> slicer;
-    PermSlicer<(FB > 1 ? FB : 2)> pslicer;
+    std::conditional_t<sizeof(R) == 8, PermSlicer64<(FB > 1 ? FB : 2)>, PermSlicer<(FB > 1 ? FB : 2)>> pslicer;
     // adaptive throughput kernel: the LDS byte offset of each element's order entry, four
     // elements per word (the lane's subcarriers do not change from symbol to symbol)
     uint32_t ocode[FB == 1 ? E / 4 : 1];
@@ -752,7 +866,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     } else if constexpr (FB > 1 && !FB_PSK_ONLY) {
         // the FFT output stays unscaled (x sqrt N); SC-OFDM adds the unscaled IFFT (x sqrt N).
         // The reference's 4/16-PSK (psk_m > 0) decide by sector and have no axis tables.
-        if (cm.psk_m == 0) pslicer.load(axis[0], (float)(scm ? cm.scale * cm.scale : cm.scale));
+        if (cm.psk_m == 0) pslicer.load(axis[0], scm ? cm.scale * cm.scale : cm.scale);
     } else if (!adaptive) {
         slicer.load(axis[0]);
     }
@@ -764,7 +878,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
     // kept channel samples of local symbol sl (zeros past the end / when ablated)
     auto load_sym = [&](int64_t sl, C (&dst)[E]) {
         const C* ys = (const C*)a.y + sl * ystride;
-        if (sl < cm.n_sym && !(a.flags & 16)) {
+        if (sl < cm.n_sym && !(flags & 16)) {
 #pragma unroll
             for (int i = 0; i < E; ++i) dst[i] = ld_stream<(FB > 0 && OFDM_RX_NT)>(ys + t + i * TPS);
         } else {
@@ -772,7 +886,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
             for (int i = 0; i < E; ++i) dst[i] = mk<R>(0, 0);
         }
     };
-    constexpr bool PF = rx_prefetch<FB, LOGN>();
+    constexpr bool PF = rx_prefetch<R, FB, LOGN>();
     C xn[PF ? E : 1];  // prefetched samples of the wave's next symbol
     if constexpr (PF) load_sym((int64_t)blockIdx.x * G::SPB + ls, xn);
 
@@ -789,9 +903,9 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
             for (int i = 0; i < E; ++i) x[i] = xn[i];
             load_sym(sl + (int64_t)gridDim.x * G::SPB, xn);  // in flight during this symbol
         }
-        if (!OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
+        if (!OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(flags & 4) || (noise && !array_noise)));
         if constexpr (!PF) load_sym(sl, x);
-        if (OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(a.flags & 4) || (noise && !array_noise)));
+        if (OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(flags & 4) || (noise && !array_noise)));
         if (OFDM_RX_NOISE_FIRST == 1 && sizeof(R) == 4 && active && noise && !array_noise) {
             // the lane's noise while the loads are in flight, then one add per element
             f32x2 nz[E];
@@ -826,7 +940,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
             for (int i = 0; i < E; ++i) {
                 const int k = t + i * TPS;
                 if (k < cp) {
-                    C v = (a.flags & 16) ? mk<R>(0, 0) : ys[N + k];
+                    C v = (flags & 16) ? mk<R>(0, 0) : ys[N + k];
                     if (array_noise) {
                         v.re += sigma * (R)a.nr[sg * (N + cp) + N + k];
                         v.im += sigma * (R)a.ni[sg * (N + cp) + N + k];
@@ -849,7 +963,7 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
                 for (int i = 0; i < E; ++i) ecoef[i] = eqa[t + i * TPS];
             }
         }
-        if (!(a.flags & 2)) fft_reg<R, LOGN, false, (FB > 0)>(x, row, tw, tw + 64, t, tt);
+        if (!(flags & 2)) fft_sym<R, LOGN, false, FB>(x, row, tw, tt, t);
         if (FB == 0) sym_sync<TPS>();  // staged words visible to the whole group
         // MMSE noise variance per OFDM symbol (equalization/models.py:39-49)
         R nv = 0;
@@ -876,14 +990,14 @@ __global__ __launch_bounds__((rx_block<FB, LOGN, EQ>()), (rx_waves<FB, LOGN, EQ>
                     x[i] = eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_PRE ? i : 0]);
             sym_sync<TPS>();  // the forward FFT has read the row
             if constexpr (FB > 1) {
-                fft_reg<R, LOGN, true, true>(x, row, tw, tw + 64, t, tt + TTS);  // 1/N in the slicer
+                fft_sym<R, LOGN, true, FB>(x, row, tw, tt + TTS, t);  // 1/N in the slicer
             } else {
                 fft_reg<R, LOGN, true, false>(x, row, tw, tw + 64, t, tt);
 #pragma unroll
                 for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
             }
         }
-        if (active && !(a.flags & 8)) {
+        if (active && !(flags & 8)) {
             const int64_t sbit = sg * cm.bps;
             const bool all_valid = FB > 1 || sbit + cm.bps <= a.n_valid_bits;
             uint32_t bes = 0, ses = 0;

@@ -260,6 +260,62 @@ __global__ __launch_bounds__(kBlock) void k_demap(DemapArgs a) {
     }
 }
 
+// ============================================================ decode + error count
+// QAMConstellationMapper.decode (constellation/models.py:251-295) / AdaptiveConstellationMapper.decode
+// (constellation/adaptive.py:203-265) followed by Simulation.run's comparison against the tx bits
+// (simulation/models.py:596-606), fused: one thread per (symbol, subcarrier) decides the nearest
+// point (per-axis slicer for the separable square-QAM LUTs, brute-force |z - C_m| with the first
+// index on ties otherwise), XORs its index with the tx bits and counts; counters[0] += bit errors
+// over stream bits < n_valid_bits, counters[1] += symbol errors (index mismatches).
+template <typename R>
+__global__ __launch_bounds__(kBlock) void k_demap_count(DemapCountArgs a) {
+    using C = cpx<R>;
+    __shared__ unsigned long long red[kBlock / 64];
+    const C* z = (const C*)a.z;
+    const int64_t n = a.n_sym * a.n_fft;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    unsigned long long be = 0, se = 0;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += stride) {
+        const int64_t s = e / a.n_fft;
+        const int k = (int)(e - s * a.n_fft);
+        int b, off, lut;
+        if (a.adaptive) {
+            const ScInfo sc = a.sc[k];
+            if (sc.lut < 0) continue;  // unused subcarrier: 0+0j on both sides
+            b = sc.bits;
+            off = sc.bitoff;
+            lut = sc.lut;
+        } else {
+            b = a.b;
+            off = k * a.b;
+            lut = 0;
+        }
+        const C v = z[e];
+        const AxisInfo& ax = a.axis[lut];
+        const uint32_t ridx = a.separable ? slice<R>(v, ax)
+                                          : (uint32_t)nn_index((double)v.re, (double)v.im, a.lut64 + 2 * ax.lut_off, 1 << b);
+        const int64_t o = s * (int64_t)a.bps + off;
+        uint32_t t = 0;
+        for (int i = 0; i < b; ++i) {
+            const int64_t p = o + i;
+            const int64_t B = p >> 3;
+            t = (t << 1) | (B < a.n_tx_bytes ? (a.tx[B] >> (7 - (int)(p & 7))) & 1u : 0u);
+        }
+        uint32_t d = ridx ^ t;
+        se += d != 0u;
+        const int64_t nvb = a.n_valid_bits - o;
+        const int keep = nvb <= 0 ? 0 : (nvb >= b ? b : (int)nvb);
+        d &= ((1u << keep) - 1u) << (b - keep);
+        be += __popc(d);
+    }
+    be = block_sum<unsigned long long>(be, red);
+    se = block_sum<unsigned long long>(se, red);
+    if (threadIdx.x == 0) {
+        if (be) atomicAdd(&a.counters[0], be);
+        if (se) atomicAdd(&a.counters[1], se);
+    }
+}
+
 // ============================================================ channel convolution
 // y[n] = sum_l h[l] s[n-l] (s[<0] = 0), truncated to len (channel/models.py:52-55);
 // per-block sum |y|^2 into partials.
@@ -330,6 +386,37 @@ __global__ __launch_bounds__(kBlock) void k_finalize(const double* partials, int
         v = op == 1 ? block_max<double>(v, red) : block_sum<double>(v, red);
         if (threadIdx.x == 0) stats[f] = op == 1 ? (v > stats[f] ? v : stats[f]) : stats[f] + v;
         __syncthreads();
+    }
+}
+
+// Fused-TX partials -> ofdm_stats: the fixed-point power limbs are summed as integers (exact, any
+// order), normalised and added to the record's limbs; power_sum is recomputed from them
+// (fx_value), so it depends only on the integer total.  sum |x|^2 (fixed order) and max |x|^2 as
+// k_finalize.
+__global__ __launch_bounds__(kBlock) void k_finalize_tx(const double* partials, int nblocks, double* stats) {
+    __shared__ double red[kBlock / 64];
+    const unsigned long long* pu = (const unsigned long long*)partials;
+    unsigned long long q0 = 0, q1 = 0;
+    double px = 0, mx = 0;
+    for (int i = threadIdx.x; i < nblocks; i += kBlock) {
+        q0 += pu[(size_t)i * kTxFields + 0];
+        q1 += pu[(size_t)i * kTxFields + 1];
+        px += partials[(size_t)i * kTxFields + 2];
+        mx = fmax(mx, partials[(size_t)i * kTxFields + 3]);
+    }
+    q0 = block_sum<unsigned long long>(q0, (unsigned long long*)red);
+    q1 = block_sum<unsigned long long>(q1, (unsigned long long*)red);
+    px = block_sum<double>(px, red);
+    mx = block_max<double>(mx, red);
+    if (threadIdx.x == 0) {
+        unsigned long long* limb = (unsigned long long*)(stats + 3);
+        unsigned long long l0 = limb[0] + q0, l1 = limb[1] + q1;
+        fx_normalize(l0, l1);
+        limb[0] = l0;
+        limb[1] = l1;
+        stats[0] = fx_value(l0, l1);
+        stats[1] += px;
+        stats[2] = fmax(stats[2], mx);
     }
 }
 

@@ -1,15 +1,22 @@
-// complex128 (parity mode / operator API) instantiation of every kernel launcher,
-// plus the precision-independent support kernels.
+// complex128 instantiation of the operator launchers (parity mode / operator API), plus the
+// precision-independent support kernels; the fused TX / RX launchers are in
+// ofdm_kernels_f64_tx.hip / ofdm_kernels_f64_rx.hip (parallel compile).
 #define OFDM_SUPPORT_KERNELS 1
 #include "ofdm_kernels_inst.hpp"
 
 namespace ofdm {
-OFDM_INSTANTIATE(double)
+OFDM_INSTANTIATE_OPS(double)
 
 hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int max_mask,
                            double* stats, hipStream_t s) {
     (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(kBlock), 0, s, partials, nblocks, nfields, max_mask, stats);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize_tx(const double* partials, int nblocks, double* stats, hipStream_t s) {
+    (void)hipGetLastError();  // stale errors were reported by their own calls
+    hipLaunchKernelGGL(k_finalize_tx, dim3(1), dim3(kBlock), 0, s, partials, nblocks, stats);
     return hipGetLastError();
 }
 

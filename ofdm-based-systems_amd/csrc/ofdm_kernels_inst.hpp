@@ -15,10 +15,13 @@ namespace ofdm {
 #ifdef OFDM_AB_ONLY
 #define OFDM_LOGN_CASES(X) X(10) X(11) X(12)
 #define OFDM_FB_CASES(X) X(6) X(8)
+#define OFDM_FB64_CASES(X) X(6) X(8)
 #else
 #define OFDM_LOGN_CASES(X) \
     X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 #define OFDM_FB_CASES(X) X(2) X(3) X(4) X(5) X(6) X(8)
+// complex128 throughput kernels: square QAM (4..256)
+#define OFDM_FB64_CASES(X) X(2) X(4) X(6) X(8)
 #endif
 
 template <typename F>
@@ -113,6 +116,15 @@ hipError_t launch_demap(const DemapArgs& a, hipStream_t s) {
 }
 
 template <typename R>
+hipError_t launch_demap_count(const DemapCountArgs& a, hipStream_t s) {
+    const int64_t n = a.n_sym * a.n_fft;
+    if (n <= 0) return hipSuccess;
+    (void)hipGetLastError();  // stale errors were reported by their own calls
+    hipLaunchKernelGGL(k_demap_count<R>, dim3(clamp_grid((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename R>
 hipError_t launch_conv(const ConvArgs& a, int grid, hipStream_t s) {
     (void)hipGetLastError();  // stale errors were reported by their own calls
     hipLaunchKernelGGL(k_conv<R>, dim3(grid), dim3(kBlock), 0, s, a);
@@ -136,7 +148,7 @@ hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
 
 template <typename R, int LOGN, int FB, int LT>
 static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
-    constexpr int BLK = tx_block<FB, LOGN, LT>();
+    constexpr int BLK = tx_block<R, FB, LOGN, LT>();
     TxArgs a = a0;
     if (FB > 0 && LT > 0) {
         // window FIR row: stream samples [-(LT-1), N+cp) at fir_pad(R0 + m)
@@ -144,7 +156,8 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
         a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
     }
     const size_t sm = smem_tx<R>(LOGN, BLK, FB > 0 ? 0 : a.c.lut_len, a.c.words_per_sym, a.L, a.slot,
-                                 FB ? tt_size(LOGN) : 0, FB > 0 && LT > 0, FB == 1 ? (size_t)4 << LOGN : 0);
+                                 uses_tt<R, LOGN, FB>() ? tt_size(LOGN) : 0, FB > 0 && LT > 0,
+                                 FB == 1 ? (size_t)4 << LOGN : 0, FB > 0, split_rows<R, FB>() && LT == 0);
     auto fn = k_tx<R, LOGN, FB, LT>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
@@ -175,6 +188,19 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
 // prefix) -> the adaptive throughput kernel (FB = 1); anything else -> the generic kernel.
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
+    if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
+        // complex128 throughput kernels: square QAM, device bits, OFDM with a cyclic prefix
+        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.nn && !a.c.scm && !a.c.zpad) {
+#define OFDM_TX_FB64(F) \
+    case F:                \
+        return tx_fast<R, LOGN, F>(a, grid, s);
+            switch (a.c.b) {
+                OFDM_FB64_CASES(OFDM_TX_FB64)
+                default: break;
+            }
+#undef OFDM_TX_FB64
+        }
+    }
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
             return tx_fast<R, LOGN, 1>(a, grid, s);
@@ -208,15 +234,17 @@ hipError_t launch_tx(int logn, const TxArgs& a, int* grid, hipStream_t s) {
 
 template <typename R, int LOGN, int EQ, int FB>
 static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
-    constexpr int BLK = rx_block<FB, LOGN, EQ>();
-    const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym, FB ? tt_size(LOGN) * (FB > 1 && a.c.scm ? 2 : 1) : 0,
+    constexpr int BLK = rx_block<R, FB, LOGN, EQ>();
+    const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym,
+                                 uses_tt<R, LOGN, FB>() ? tt_size(LOGN) * (FB > 1 && a.c.scm ? 2 : 1) : 0,
                                  (FB == 1 ? 8 * sizeof(OrderParams) : 0) +
-                                     (eq_in_lds<FB, LOGN, EQ>() ? ((size_t)2 * sizeof(R)) << LOGN : 0));
+                                     (eq_in_lds<FB, LOGN, EQ>() ? ((size_t)2 * sizeof(R)) << LOGN : 0),
+                                 FB > 0, split_rows<R, FB>());
     auto fn = k_rx<R, LOGN, EQ, FB>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
-    if (rx_prefetch<FB, LOGN>() || (OFDM_PERSISTENT && FB > 0)) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
+    if (rx_prefetch<R, FB, LOGN>() || (OFDM_PERSISTENT && FB > 0)) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
@@ -233,6 +261,19 @@ static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
 // equaliser; anything else -> the generic kernel.
 template <typename R, int LOGN>
 static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
+    if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
+        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr && !a.c.nn && !a.c.scm &&
+            !a.c.zpad) {
+#define OFDM_RX_FB64(F) \
+    case F:                \
+        return rx_eq<R, LOGN, F>(a, grid, s);
+            switch (a.c.b) {
+                OFDM_FB64_CASES(OFDM_RX_FB64)
+                default: break;
+            }
+#undef OFDM_RX_FB64
+        }
+    }
     if constexpr (sizeof(R) == 4 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
             !a.c.scm && !a.c.zpad && !a.c.nn)
@@ -272,6 +313,7 @@ hipError_t launch_rx(int logn, const RxArgs& a, int* grid, hipStream_t s) {
     template hipError_t launch_equalize<R>(const EqArgs&, hipStream_t);             \
     template hipError_t launch_map<R>(const MapArgs&, hipStream_t);                 \
     template hipError_t launch_demap<R>(const DemapArgs&, hipStream_t);             \
+    template hipError_t launch_demap_count<R>(const DemapCountArgs&, hipStream_t);  \
     template hipError_t launch_conv<R>(const ConvArgs&, int, hipStream_t);          \
     template hipError_t launch_power<R>(const PowerArgs&, int, hipStream_t);        \
     template hipError_t launch_awgn<R>(const AwgnArgs&, hipStream_t);

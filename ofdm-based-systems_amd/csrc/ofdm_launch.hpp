@@ -8,9 +8,20 @@
 #include "ofdm_device.hpp"
 #include "ofdm_hip.h"
 
+// Diagnostic ablation switches (timing studies: tools/ablate.py, tools/power_probe.py) exist only in
+// builds made with `make VARIANT=ablate EXTRA=-DOFDM_ABLATION=1`; the product library compiles
+// every switch out of the kernels and never reads OFDM_ABLATE_TX / OFDM_ABLATE_RX.
+#ifndef OFDM_ABLATION
+#define OFDM_ABLATION 0
+#endif
+
 namespace ofdm {
 
+__host__ __device__ constexpr int ablation_flags(int f) { return OFDM_ABLATION ? f : 0; }
+
 constexpr int kMaxGrid = 4096;  // partial-sum workspace rows
+// fused TX partials per workgroup: sum |y|^2 as fixed-point limbs (2 x u64), sum |x|^2, max |x|^2
+constexpr int kTxFields = 4;
 constexpr int kMaxTaps = 32;
 constexpr int kMaxLut = 512;
 
@@ -55,6 +66,18 @@ struct DemapArgs {
     const AxisInfo* axis;
     const int32_t* active;
     const double* lut64;
+};
+
+struct DemapCountArgs {
+    const void* z;            // (n_sym, N) equalised symbols
+    const uint8_t* tx;        // packed tx bits, OFDM symbol s at bit s * bps
+    int64_t n_sym, n_valid_bits, n_tx_bytes;
+    int n_fft, b, bps, adaptive, separable;
+    const ScInfo* sc;
+    const AxisInfo* axis;
+    const double* lut64;
+    int lut_len;
+    unsigned long long* counters;
 };
 
 struct ConvArgs {
@@ -116,7 +139,8 @@ struct TxArgs {
     int L;
     int chunk;
     int slot;   // complex elements per symbol row in LDS
-    int flags;  // diagnostic ablation (OFDM_ABLATE_TX): 1 no bit staging, 2 no FFT, 4 no y store
+    int flags;  // diagnostic ablation (OFDM_ABLATION builds, OFDM_ABLATE_TX): 1 no bit staging, 2 no FFT,
+                // 4 no y store
 };
 
 struct RxArgs {
@@ -132,7 +156,7 @@ struct RxArgs {
     uint64_t* counters;
     void* z_out;
     int64_t z_keep;
-    int flags;  // diagnostic ablation (OFDM_ABLATE_RX): 1 no noise, 2 no FFT, 4 no bit staging,
+    int flags;  // diagnostic ablation (OFDM_ABLATION builds, OFDM_ABLATE_RX): 1 no noise, 2 no FFT, 4 no bit staging,
                 // 8 no equalise/demap/compare, 16 no y load
 };
 
@@ -155,29 +179,32 @@ inline int tx_slot(int logn, int cp, int L) {
     const int ext = (1 << logn) + cp + (L > 1 ? L - 1 : 0);
     return geo_padn(logn) > ext ? geo_padn(logn) : ext;
 }
-// fused kernels, blk threads; tts = per-pass twiddle entries (throughput kernels) or 0
-// (the throughput kernels, tts > 0, carve no two-level twiddles and no staged bit words)
+// fused kernels, blk threads; tts = per-pass twiddle entries (0: the two-level table instead);
+// fast = throughput kernel (no staged bit words); row_real = rows of reals (complex128
+// throughput kernels, fft_reg_split) instead of complex rows
 template <typename R>
 inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int slot, int tts, bool wfir,
-                      size_t extra = 0 /* adaptive throughput kernel: per-subcarrier table */) {
+                      size_t extra /* adaptive throughput kernel: per-subcarrier table */, bool fast, bool row_real) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn, blk);
     const int tls = L > 1 ? L - 1 : 1;
-    if (tts > 0) wps = 0;
+    if (fast) wps = 0;
     return rnd16((tts > 0 ? 0 : 128) * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(wfir ? 32 * c : 0) +
            rnd16(4 * sizeof(AxisInfo)) +
-           rnd16((size_t)spb * slot * c) + rnd16((size_t)spb * tls * c) +
+           rnd16((size_t)spb * slot * (row_real ? sizeof(R) : c)) + rnd16((size_t)spb * tls * c) +
            rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(double)) + rnd16((size_t)tts * c) +
            rnd16(extra);
 }
 template <typename R>
-inline size_t smem_rx(int logn, int blk, int wps, int tts, size_t extra = 0 /* adaptive: order table */) {
+inline size_t smem_rx(int logn, int blk, int wps, int tts, size_t extra /* adaptive: order table */, bool fast,
+                      bool row_real) {
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn, blk);
-    if (tts > 0) wps = 0;
-    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16(4 * sizeof(AxisInfo)) + rnd16((size_t)spb * geo_padn(logn) * c) +
-           rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(R)) +
-           rnd16((size_t)(blk / 64) * sizeof(unsigned long long)) + rnd16((size_t)tts * c) + rnd16(extra);
+    if (fast) wps = 0;
+    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16(4 * sizeof(AxisInfo)) +
+           rnd16((size_t)spb * geo_padn(logn) * (row_real ? sizeof(R) : c)) + rnd16((size_t)spb * wps * 4) +
+           rnd16((size_t)(blk / 64) * sizeof(R)) + rnd16((size_t)(blk / 64) * sizeof(unsigned long long)) +
+           rnd16((size_t)tts * c) + rnd16(extra);
 }
 
 // ---- launchers (instantiated for float and double in ofdm_kernels_f{32,64}.hip)
@@ -189,6 +216,8 @@ template <typename R>
 hipError_t launch_map(const MapArgs& a, hipStream_t s);
 template <typename R>
 hipError_t launch_demap(const DemapArgs& a, hipStream_t s);
+template <typename R>
+hipError_t launch_demap_count(const DemapCountArgs& a, hipStream_t s);
 template <typename R>
 hipError_t launch_conv(const ConvArgs& a, int grid, hipStream_t s);
 template <typename R>
@@ -203,6 +232,8 @@ hipError_t launch_rx(int logn, const RxArgs& a, int* grid, hipStream_t s);
 
 hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int max_mask,
                            double* stats, hipStream_t s);
+// the fused TX's partials into an ofdm_stats record (exact fixed-point power, ofdm_hip.h)
+hipError_t launch_finalize_tx(const double* partials, int nblocks, double* stats, hipStream_t s);
 hipError_t launch_nn_classify(const double* lut, int m, const double* z, int64_t n, int64_t* idx,
                               hipStream_t s);
 

@@ -24,9 +24,12 @@ import torch
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
                          "libofdm_hip%s.so" % ("_" + os.environ["OFDM_LIB_VARIANT"]
                                                if os.environ.get("OFDM_LIB_VARIANT") else ""))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OFDM_F32, OFDM_F64 = 0, 1
+# ofdm_stats (include/ofdm_hip.h): power_sum, x_power_sum, x_peak (double), power_fx[2] (int64)
+STATS_WORDS = 5
+FX_HI, FX_LO = 2.0 ** -8, 2.0 ** -40
 EQ_NONE, EQ_ZF, EQ_MMSE = 0, 1, 2
 PREFIX_CYCLIC, PREFIX_ZERO = 0, 1
 MOD_OFDM, MOD_SC = 0, 1
@@ -87,6 +90,7 @@ SIGNATURES = {
     "ofdm_fft": (ctypes.c_int, [_VP, _VP, _VP, _I64, _I32]),
     "ofdm_map": (ctypes.c_int, [_VP, _VP, _VP, _I64, _I64, _VP]),
     "ofdm_demap": (ctypes.c_int, [_VP, _VP, _VP, _I64, _VP]),
+    "ofdm_demap_count": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
     "ofdm_nn_classify": (ctypes.c_int, [_VP, _VP, _I32, _VP, _I64, _VP]),
     "ofdm_modulate": (ctypes.c_int, [_VP, _VP, _VP, _I64, _VP]),
     "ofdm_demodulate": (ctypes.c_int, [_VP, _VP, _VP, _I64, _F64, _VP]),

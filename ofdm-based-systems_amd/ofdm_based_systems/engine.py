@@ -20,8 +20,9 @@ Bit / noise sources:
     touches HBM and results do not depend on the number of GPUs.
 
 Multi-GPU: symbols [r*S/R, (r+1)*S/R) go to rank r; the only exchanges are one
-all-gather of three doubles per rank (the AWGN power is a whole-stream mean,
-noise/models.py:14) and one all-reduce of the two u64 counters.
+all-gather of the 40-byte ofdm_stats record per rank (the AWGN power is a whole-stream
+mean, noise/models.py:14, kept as an exact fixed-point sum so that sigma does not depend
+on the rank count) and one all-reduce of the two u64 counters.
 """
 
 from __future__ import annotations
@@ -50,6 +51,29 @@ class LinkStats:
     papr_db: float
     received: Optional[np.ndarray] = None
     timings: dict = field(default_factory=dict)
+
+
+def new_stats(dev) -> torch.Tensor:
+    """A zeroed ofdm_stats record (include/ofdm_hip.h): power_sum, x_power_sum, x_peak as
+    float64 and the two int64 fixed-point limbs of sum |y|^2, 5 x 8 bytes."""
+    return torch.zeros(B.STATS_WORDS, dtype=torch.float64, device=dev)
+
+
+def combine_stats(stats: torch.Tensor, parts) -> None:
+    """Reduce every rank's ofdm_stats record into ``stats`` (the same on every rank): the
+    fixed-point power limbs add as integers -- exact, so power_sum and sigma equal the
+    single-GPU values bit for bit -- then power_sum is recomputed from them as the kernels do;
+    sum |x|^2 adds in rank order, max |x|^2 is the maximum."""
+    g = torch.stack(list(parts))                      # (world, 5) float64
+    limbs = g.view(torch.int64)[:, 3:5].sum(0)        # exact
+    l0 = limbs[0] & 0xFFFFFFFF
+    l1 = limbs[1] + (limbs[0] >> 32)
+    si = stats.view(torch.int64)
+    si[3] = l0
+    si[4] = l1
+    stats[0] = l1.to(torch.float64) * B.FX_HI + l0.to(torch.float64) * B.FX_LO
+    stats[1] = g[:, 1].sum()
+    stats[2] = g[:, 2].max()
 
 
 def shard(n: int, rank: int, world: int) -> tuple:
@@ -163,7 +187,7 @@ class LinkEngine:
             nr_d = self.upload(np.asarray(normals[0], np.float64))
             ni_d = self.upload(np.asarray(normals[1], np.float64))
 
-        stats = torch.zeros(3, dtype=torch.float64, device=dev)
+        stats = new_stats(dev)
         counters = torch.zeros(2, dtype=torch.int64, device=dev)
         csize = 8 if self.cdtype == torch.complex64 else 16
         per_batch = batch or max(1, min(mine, y_budget // (self.ystride * csize)))
@@ -172,16 +196,14 @@ class LinkEngine:
 
         def reduce_stats():
             # one collective on the TX -> RX critical path: every rank gathers all ranks'
-            # (sum|y|^2, sum|x|^2, max|x|^2) and reduces them in rank order, so all ranks hold
-            # bit-identical statistics (and sigma)
+            # ofdm_stats records and reduces them (combine_stats), so all ranks hold the
+            # statistics -- and sigma -- of a single-GPU run, bit for bit
             if world > 1:
                 import torch.distributed as dist
 
                 parts = [torch.empty_like(stats) for _ in range(world)]
                 dist.all_gather(parts, stats, group=group)
-                g = torch.stack(parts)
-                stats[:2].copy_(g[:, :2].sum(0))
-                stats[2:].copy_(g[:, 2:].amax(0))
+                combine_stats(stats, parts)
 
         if per_batch >= mine:
             # whole shard resident: one TX, one RX
@@ -195,7 +217,7 @@ class LinkEngine:
             # power pass first (the AWGN power is a whole-stream mean), then TX+RX per batch
             self.tx(stream, bits_d, seed, lo, mine, None, stats)
             reduce_stats()
-            scratch = torch.zeros(3, dtype=torch.float64, device=dev)
+            scratch = new_stats(dev)
             y = torch.empty((per_batch, self.ystride), dtype=self.cdtype, device=dev)
             for b0 in range(lo, hi, per_batch):
                 nb = min(per_batch, hi - b0)
@@ -218,13 +240,14 @@ class LinkEngine:
 
 
     def run_pipelined(self, n_sym: int, snr_db: float, seeds, *, group=None,
-                      events: Optional[list] = None) -> list:
+                      events: Optional[list] = None, y_budget: int = DEFAULT_Y_BUDGET) -> list:
         """Independent throughput-mode runs (one per seed) of global OFDM symbols [0, n_sym),
         software-pipelined across runs: run k+1's TX is enqueued before run k's RX, so with
         several ranks the statistics exchange of run k (the one collective on a run's
         TX -> RX path) is in flight while the GPU transmits run k+1.  Every run is complete
         and its counts are those of :meth:`run_async` with the same seed; returns the
-        PendingLink of each run."""
+        PendingLink of each run.  Two runs' channel samples are live at once; when they do not
+        fit ``y_budget`` the runs go through :meth:`run_async` one after another (batched)."""
         dev = self.device()
         stream = self.stream()
         world, rank = 1, 0
@@ -237,9 +260,13 @@ class LinkEngine:
         N, cp = self.n_fft, self.cp
         samples = n_sym * (N + cp)
         n_valid = self.valid_bits(n_sym)
+        csize = 8 if self.cdtype == torch.complex64 else 16
+        if 2 * max(mine, 1) * self.ystride * csize > y_budget:
+            return [self.run_async(n_sym, snr_db, seed=s, group=group, events=events, y_budget=y_budget)
+                    for s in seeds]
 
         def tx(seed):
-            stats = torch.zeros(3, dtype=torch.float64, device=dev)
+            stats = new_stats(dev)
             y = torch.empty((max(mine, 1), self.ystride), dtype=self.cdtype, device=dev)
             self._timed(events, "ofdm_tx", mine, lambda: self.tx(stream, None, seed, lo, mine, y, stats))
             work = None
@@ -252,11 +279,9 @@ class LinkEngine:
 
         def rx(state):
             seed, y, stats, work = state
-            if work is not None:  # reduce the gathered statistics in rank order (as run_async)
+            if work is not None:  # reduce the gathered statistics (as run_async)
                 work[0].wait()
-                g = torch.stack(work[1])
-                stats[:2].copy_(g[:, :2].sum(0))
-                stats[2:].copy_(g[:, 2:].amax(0))
+                combine_stats(stats, work[1])
             counters = torch.zeros(2, dtype=torch.int64, device=dev)
             self._timed(events, "ofdm_rx", mine, lambda: self.rx(
                 stream, y, None, None, seed, stats, samples, snr_db, True, None, lo, mine, n_valid, counters))

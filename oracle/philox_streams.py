@@ -37,6 +37,7 @@ per lane, TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS 
 from __future__ import annotations
 
 from dataclasses import dataclass
+from typing import Optional
 
 import numpy as np
 
@@ -122,13 +123,26 @@ def noise_table(sigma: float) -> np.ndarray:
     return re.astype(np.float64) + 1j * im.astype(np.float64)
 
 
-def noise_from_words(w: np.ndarray, sigma: float) -> np.ndarray:
+def noise_from_words(w: np.ndarray, sigma: float, with_bound: bool = False):
     """Complex normal of each 32-bit lane word (radius from the word with bits 3..8 set,
-    phase = bits 3..8 through the table)."""
+    phase = bits 3..8 through the table).
+
+    with_bound: also return a bound on |GPU noise - this value| per word.  The GPU evaluates
+    log2 and sqrt with the float32 hardware instructions: log2 within 2 ulp of its float32 result
+    (<= 2^-18 absolute for arguments < 2^32), the subtraction from 32 and the square root within
+    1 ulp, the product with the table entry within 1/2 ulp per component.  With A = 32 - log2(f)
+    and dA = 2^-18 + 2^-23 A, the radius error is at most min(dA / sqrt(A), sqrt(dA)) + 2^-23 r."""
     w = np.asarray(w, np.uint32)
     f = (w | NOISE_MASK).astype(np.float32)  # round to nearest even, as v_cvt_f32_u32
-    r = np.sqrt(32.0 - np.log2(f.astype(np.float64)))
-    return r * noise_table(sigma)[(w >> np.uint32(3)) & np.uint32(NOISE_PHASES - 1)]
+    A = 32.0 - np.log2(f.astype(np.float64))
+    r = np.sqrt(A)
+    e = noise_table(sigma)[(w >> np.uint32(3)) & np.uint32(NOISE_PHASES - 1)]
+    n = r * e
+    if not with_bound:
+        return n
+    dA = 2.0 ** -18 + 2.0 ** -23 * A
+    dr = np.minimum(dA / np.maximum(np.sqrt(A), 1e-300), np.sqrt(dA)) + 2.0 ** -23 * r
+    return n, dr * np.abs(e) + 2.0 ** -23 * np.abs(n)
 
 
 def _lane_to_row(v: np.ndarray, S: int, N: int) -> np.ndarray:
@@ -148,11 +162,15 @@ def tx_indices(gen: LaneStream, S: int, N: int, b) -> np.ndarray:
     return _lane_to_row(byte.astype(np.int64), S, N) & mask[None, :]
 
 
-def lane_noise(gen: LaneStream, S: int, N: int, sigma: float) -> np.ndarray:
-    """Complex noise (S, N) at the kept time samples, from outputs m2 .. m(E+1) of every lane."""
+def lane_noise(gen: LaneStream, S: int, N: int, sigma: float, with_bound: bool = False):
+    """Complex noise (S, N) at the kept time samples, from outputs m2 .. m(E+1) of every lane
+    (with_bound: and the (S, N) bound of noise_from_words)."""
     E, _ = geometry(N)
-    n = np.stack([noise_from_words(gen.next(), sigma) for _ in range(E)], axis=1)
-    return _lane_to_row(n, S, N)
+    parts = [noise_from_words(gen.next(), sigma, with_bound) for _ in range(E)]
+    if not with_bound:
+        return _lane_to_row(np.stack(parts, axis=1), S, N)
+    return (_lane_to_row(np.stack([p[0] for p in parts], axis=1), S, N),
+            _lane_to_row(np.stack([p[1] for p in parts], axis=1), S, N))
 
 
 @dataclass
@@ -164,11 +182,14 @@ class PhiloxLink:
     x_peak: float
     idx: np.ndarray        # (S, N) tx constellation indices
     y: np.ndarray          # stored channel samples before noise: (S, N) kept, or (S, N+cp) with ZP
+    # (bit_lo, bit_hi, sym_lo, sym_hi): the error counts of every decision consistent with the
+    # GPU's deviation from this restatement (decision_bracket), when run_philox(precision=...)
+    bracket: Optional[tuple] = None
 
 
 def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq: str, snr_db: float,
                noise_on: bool = True, modulator: str = "OFDM", prefix: str = "CP",
-               scheme: str = "QAM", orders=None) -> PhiloxLink:
+               scheme: str = "QAM", orders=None, precision: Optional[str] = None) -> PhiloxLink:
     """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic.
 
     modulator "OFDM" | "SC" (modulation/models.py:58-91), prefix "CP" | "ZP"
@@ -180,9 +201,13 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     ignored).  As in the reference's decode (constellation/adaptive.py:259-263) a trailing
     partial byte of the whole run's bit stream is not compared; symbol errors count every
     used subcarrier.
+
+    precision "f32" | "f64": also return the decision bracket of a GPU run in that arithmetic
+    (PhiloxLink.bracket, see decision_bracket).
     """
     E, tps = geometry(N)
     gen = lane_generators(seed, np.arange(S), N)
+    want_bound = precision is not None and noise_on
     if orders is not None:
         orders = np.asarray(orders, np.int64)
         bk = np.array([int(np.log2(o)) if o > 0 else 0 for o in orders], np.int64)
@@ -211,49 +236,201 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     else:
         yk, tail = y[:, cp:].copy(), None
     rxs = yk.copy()
+    nerr = np.zeros(S)  # per symbol: sum over its received samples of the noise deviation bound
     if noise_on:
         p = py / (S * (N + cp))
         sigma = np.sqrt((p / 10 ** (snr_db / 10)) / 2.0)
-        rxs = rxs + lane_noise(gen, S, N, sigma)
+        if want_bound:
+            nz, nb = lane_noise(gen, S, N, sigma, with_bound=True)
+            nerr += nb.sum(axis=1)
+        else:
+            nz = lane_noise(gen, S, N, sigma)
+        rxs = rxs + nz
     if prefix == "ZP" and cp > 0:
         if noise_on:
             t = np.tile(np.arange(tps), S)
             for i in range(E):
                 k = t + i * tps
-                n = lane_noise_tail(gen, sigma)
+                w = gen.next()
+                n, nb = noise_from_words(w, sigma, with_bound=True)
                 use = k < cp
                 srow = np.repeat(np.arange(S), tps)[use]
                 tail[srow, k[use]] += n[use]
+                np.add.at(nerr, srow, nb[use])
         rxs[:, :cp] += tail
     H = np.fft.fft(np.asarray(h_raw, np.complex128), N)
-    Z = O.equalize(np.fft.fft(rxs, axis=1, norm="ortho"), H, eq, snr_db)
+    Y = np.fft.fft(rxs, axis=1, norm="ortho")
+    Z = O.equalize(Y, H, eq, snr_db)
     if modulator == "SC":
         Z = np.fft.ifft(Z, axis=1, norm="ortho")
+    bracket = None
+    if precision is not None:
+        delta = z_error_bound(precision, Y, H, eq, snr_db, nerr, modulator, N)
+        if orders is not None:
+            bracket = adaptive_bracket(Z, idx, orders, bk, delta)
+        else:
+            bracket = decision_bracket(Z, idx, lut, b, delta, scheme)
     if orders is not None:
         ridx = np.zeros((S, N), np.int64)
         for o, lt in luts.items():
             cols = np.flatnonzero(orders == o)
             ridx[:, cols] = O.nn_demap(Z[:, cols].ravel(), lt).reshape(S, len(cols))
         diff = (ridx ^ idx).astype(np.int64)
-        # stream position of bit j (MSB first) of subcarrier k in symbol s: s*tot + off_k + j
-        tot = int(bk.sum())
-        valid = (S * tot // 8) * 8
-        off = np.concatenate([[0], np.cumsum(bk)[:-1]])
-        be = 0
-        for j in range(int(bk.max(initial=0))):
-            has = bk > j
-            bit = (diff >> np.maximum(bk - 1 - j, 0)[None, :]) & 1
-            pos = np.arange(S)[:, None] * tot + (off + j)[None, :]
-            be += int(np.count_nonzero(bit.astype(bool) & has[None, :] & (pos < valid)))
-        se = int(np.count_nonzero(diff[:, bk > 0]))
-        return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk)
+        be, se = adaptive_counts(diff, bk, S)
+        return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk, bracket)
     ridx = O.nn_demap(Z.ravel(), lut).reshape(S, N)
     diff = (ridx ^ idx).astype(np.uint64)
     be = int(sum(int(np.count_nonzero((diff >> np.uint64(j)) & np.uint64(1))) for j in range(b)))
     se = int(np.count_nonzero(ridx != idx))
-    return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk)
+    return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk, bracket)
 
 
-def lane_noise_tail(gen: LaneStream, sigma: float) -> np.ndarray:
-    """One noise word per lane (all lanes draw; only lanes owning a tail sample use it)."""
-    return noise_from_words(gen.next(), sigma)
+def adaptive_counts(diff: np.ndarray, bk: np.ndarray, S: int):
+    """Bit / symbol errors of CAPACITY_BASED decisions (diff = rx ^ tx index per (s, k)): the
+    stream position of bit j (MSB first) of subcarrier k in symbol s is s*tot + off_k + j, and a
+    trailing partial byte of the run is not compared (constellation/adaptive.py:259-263)."""
+    tot = int(bk.sum())
+    valid = (S * tot // 8) * 8
+    off = np.concatenate([[0], np.cumsum(bk)[:-1]])
+    be = 0
+    for j in range(int(bk.max(initial=0))):
+        has = bk > j
+        bit = (diff >> np.maximum(bk - 1 - j, 0)[None, :]) & 1
+        pos = np.arange(S)[:, None] * tot + (off + j)[None, :]
+        be += int(np.count_nonzero(bit.astype(bool) & has[None, :] & (pos < valid)))
+    se = int(np.count_nonzero(diff[:, bk > 0]))
+    return be, se
+
+
+# --------------------------------------------------------------------------- decision brackets
+# A GPU run and this restatement see the same bits and the same noise words, but not bit-identical
+# received points: the GPU evaluates the noise radius with float32 hardware log2 / sqrt (bounded per
+# word by noise_from_words) and runs its FFTs in its own arithmetic.  z_error_bound turns these into
+# a bound on |Z_gpu - Z| per element; decision_bracket then counts the errors of every decision
+# consistent with that bound.  A correct kernel's integer counts lie inside [lo, hi]; the bracket
+# is empty of slack (lo = hi) unless a received point lies within the bound of a decision boundary.
+
+def z_error_bound(precision: str, Y: np.ndarray, H: np.ndarray, eq: str, snr_db: float,
+                  noise_err: np.ndarray, modulator: str, N: int) -> np.ndarray:
+    """(S, N) bound on the deviation of the GPU's equalised points from this restatement's.
+
+    * noise: each received sample deviates by at most its noise_from_words bound; through the
+      ortho FFT a subcarrier deviates by at most the sum over the symbol's samples / sqrt(N);
+    * arithmetic: the FFT / FIR rounding of the kernel, bounded through the 2-norm, c log2(N) u
+      sqrt(N) rms(Y) per symbol (u = 2^-24 complex64 with c = 6 for the TX and RX transforms and
+      the FIR, u = 2^-53 complex128);
+    * equaliser: the deviation times the subcarrier's gain |dZ/dY| (ZF 1/|H|, MMSE
+      |H| / (|H|^2 + nv)), plus a relative term for the MMSE noise variance computed from the
+      GPU's own received power;
+    * single carrier: the IFFT after the equaliser preserves the 2-norm, so the bound is the
+      2-norm of the per-subcarrier bounds."""
+    S = Y.shape[0]
+    logn = max(1.0, np.log2(N))
+    u = 2.0 ** -24 if precision == "f32" else 2.0 ** -53
+    rms = np.sqrt(np.mean(np.abs(Y) ** 2, axis=1))
+    dy = noise_err / np.sqrt(N) + 6.0 * logn * u * np.sqrt(N) * rms  # (S,)
+    if eq == "NONE":
+        g = np.ones((S, N))
+        rel = 0.0
+    elif eq == "ZF":
+        h = np.where(H == 0, 1e-10, H)
+        g = np.broadcast_to(1.0 / np.abs(h), (S, N))
+        rel = 4 * u
+    else:
+        gm = np.mean(np.abs(H) ** 2)
+        nv = (np.mean(np.abs(Y) ** 2, axis=1) / 10 ** (snr_db / 10)) / gm
+        g = np.abs(H)[None, :] / (np.abs(H)[None, :] ** 2 + nv[:, None])
+        # nv from the GPU's received power: relative deviation <= 2 dy / rms + rounding
+        rel = 8 * u + 2 * np.max(dy / np.maximum(rms, 1e-300))
+    Zabs = np.abs(Y) * g
+    d = g * dy[:, None] + rel * Zabs + 1e-300
+    if modulator == "SC":
+        d = np.broadcast_to(np.sqrt(np.sum(d ** 2, axis=1))[:, None], (S, N))
+    return np.asarray(d)
+
+
+def _qam_levels(lut: np.ndarray):
+    """Sorted axis levels, their step and the (kq, ki) -> index table of a square-QAM LUT."""
+    lev = np.unique(np.round(lut.real, 12))
+    side = len(lev)
+    table = np.zeros((side, side), np.int64)
+    ki = np.searchsorted(lev, np.round(lut.real, 12))
+    kq = np.searchsorted(lev, np.round(lut.imag, 12))
+    table[kq, ki] = np.arange(len(lut))
+    return lev, lev[1] - lev[0], table
+
+
+def _axis_candidates(u: np.ndarray, lev0: float, step: float, side: int, d: np.ndarray):
+    """Decided level of each coordinate and the alternative level across the nearest interior
+    threshold when the coordinate lies within d of it (else the decided level again)."""
+    y = (u - lev0) / step
+    k = np.clip(np.rint(y), 0, side - 1).astype(np.int64)
+    if side < 2:
+        return k, k
+    th = np.clip(np.floor(y), 0, side - 2) + 0.5
+    near = np.abs(y - th) * step <= d
+    alt = np.where(k <= th, th + 0.5, th - 0.5).astype(np.int64)
+    return k, np.where(near, alt, k)
+
+
+def _popcount(v: np.ndarray) -> np.ndarray:
+    return np.bitwise_count(np.asarray(v, np.uint64)).astype(np.int64)
+
+
+def decision_bracket(Z: np.ndarray, idx: np.ndarray, lut: np.ndarray, b: int, delta: np.ndarray,
+                     scheme: str = "QAM") -> tuple:
+    """(bit_lo, bit_hi, sym_lo, sym_hi) over every decision of points within delta of Z.
+
+    QAM (the reference's square LUTs are separable): per axis the decided level
+    and, near an interior threshold, the level across it -- up to four candidate points.  PSK
+    (LUT[gray(i)] = exp(2 pi j i / M), constellation/models.py:356-380): the decided sector and,
+    when the point lies within delta of a sector boundary ray, the sector across it."""
+    Z = np.asarray(Z).ravel()
+    idx = np.asarray(idx).ravel().astype(np.int64)
+    d = np.broadcast_to(delta, np.asarray(delta).shape).ravel()
+    if scheme == "PSK":
+        M = len(lut)
+        w = 2 * np.pi / M
+        th = np.mod(np.angle(Z), 2 * np.pi)
+        k = np.mod(np.rint(th / w), M).astype(np.int64)
+        off = th - np.rint(th / w) * w                 # angle from the decided point, |off| <= w/2
+        dist = np.abs(Z) * np.sin(np.abs(np.abs(off) - w / 2))  # distance to the nearer boundary ray
+        near = (dist <= d) & (M > 1)
+        alt = np.mod(k + np.where(off >= 0, 1, -1), M)
+        gray = lambda v: v ^ (v >> 1)  # noqa: E731
+        cands = [gray(k), np.where(near, gray(alt), gray(k))]
+    else:
+        lev, step, table = _qam_levels(lut)
+        side = len(lev)
+        ki, ki2 = _axis_candidates(Z.real, lev[0], step, side, d)
+        kq, kq2 = _axis_candidates(Z.imag, lev[0], step, side, d)
+        cands = [table[kq, ki], table[kq, ki2], table[kq2, ki], table[kq2, ki2]]
+    be = np.stack([_popcount(c ^ idx) for c in cands])
+    ne = np.stack([c != idx for c in cands])
+    return (int(be.min(0).sum()), int(be.max(0).sum()), int(ne.all(0).sum()), int(ne.any(0).sum()))
+
+
+def adaptive_bracket(Z: np.ndarray, idx: np.ndarray, orders: np.ndarray, bk: np.ndarray,
+                     delta: np.ndarray) -> tuple:
+    """decision_bracket for CAPACITY_BASED loading: per order, the QAM candidates of its
+    subcarriers; bit errors counted as adaptive_counts does (trailing partial byte excluded)."""
+    S, N = Z.shape
+    d = np.broadcast_to(delta, (S, N))
+    cand = [np.array(idx, np.int64) for _ in range(4)]
+    for o in np.unique(orders):
+        if o <= 0:
+            continue
+        cols = np.flatnonzero(orders == o)
+        lev, step, table = _qam_levels(O.qam_lut(int(o)))
+        zz, dd = Z[:, cols], d[:, cols]
+        ki, ki2 = _axis_candidates(zz.real, lev[0], step, len(lev), dd)
+        kq, kq2 = _axis_candidates(zz.imag, lev[0], step, len(lev), dd)
+        for c, (a_, b_) in zip(cand, ((kq, ki), (kq, ki2), (kq2, ki), (kq2, ki2))):
+            c[:, cols] = table[a_, b_]
+    be0, _ = adaptive_counts((cand[0] ^ idx).astype(np.int64), bk, S)
+    # the other candidates change an element's bit count by at most the spread of its popcounts
+    diffs = np.stack([_popcount(c ^ idx) for c in cand])
+    used = (bk > 0)[None, :]
+    slack = int(np.where(used, diffs.max(0) - diffs.min(0), 0).sum())
+    ne = np.stack([(c != idx) & used for c in cand])
+    return (be0 - slack, be0 + slack, int(ne.all(0).sum()), int(ne.any(0).sum()))

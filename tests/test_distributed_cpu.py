@@ -7,6 +7,7 @@ counter all-reduce -- is the production LinkEngine.run.  The sharded result must
 the single-process oracle run bit for bit.
 """
 
+import math
 import os
 import socket
 
@@ -19,6 +20,19 @@ from conftest import channel
 
 import ofdm_oracle as O
 from ofdm_based_systems.engine import LinkEngine, shard
+
+
+def fx_add(stats: torch.Tensor, p: float) -> None:
+    """Add one symbol's sum |y|^2 to an ofdm_stats record the way the kernels do (fx_accum:
+    2^-40 fixed point in 32-bit limbs, normalised; power_sum recomputed from the limbs)."""
+    a = p * 256.0
+    hi = math.floor(a)
+    lo = round((a - hi) * 2.0 ** 32)  # round half to even, as rint
+    si = stats.view(torch.int64)
+    l0, l1 = int(si[3]) + lo, int(si[4]) + hi
+    l1, l0 = l1 + (l0 >> 32), l0 & 0xFFFFFFFF
+    si[3], si[4] = l0, l1
+    stats[0] = l1 * 2.0 ** -8 + l0 * 2.0 ** -40
 
 
 class OracleEngine(LinkEngine):
@@ -67,7 +81,7 @@ class OracleEngine(LinkEngine):
             ext = self._ext(bits_d, s)
             prev = self._ext(bits_d, s - 1)[len(ext) - (L - 1):] if L > 1 else np.zeros(0)
             full = np.convolve(np.concatenate([prev, ext]), self.hn)[L - 1:L - 1 + len(ext)]
-            stats[0] += float(np.sum(np.abs(full) ** 2))
+            fx_add(stats, float(np.sum(np.abs(full) ** 2)))
             stats[1] += float(np.sum(np.abs(ext) ** 2))
             stats[2] = max(float(stats[2]), float(np.max(np.abs(ext) ** 2)))
             if y is not None:
@@ -134,7 +148,10 @@ def test_sharded_engine_matches_single_process_oracle(world, batch):
         be, se, papr, _ = out[r]
         assert (be, se) == (ref.bit_errors, ref.symbol_errors), (r, be, se, ref)
         assert abs(papr - ref.papr_db) < 1e-9
-    assert len({out[r][3] for r in range(world)}) == 1  # every rank saw the same global power
+    # every rank holds the power of the single-process run, bit for bit (exact fixed-point sum)
+    single = OracleEngine(c["N"], c["M"], h, cp, c["eq"]).run(
+        c["S"], c["snr"], bits=np.frombuffer(tx, np.uint8), normals=nz, batch=batch)
+    assert {out[r][3] for r in range(world)} == {single.power_sum}
 
 
 def _pipelined_worker(rank, world, port, out):

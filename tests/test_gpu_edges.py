@@ -15,7 +15,7 @@ from conftest import channel
 import philox_streams as P
 import ofdm_oracle as O
 from ofdm_based_systems import _backend as B
-from ofdm_based_systems.engine import LinkEngine
+from ofdm_based_systems.engine import LinkEngine, new_stats
 
 pytestmark = pytest.mark.gpu
 
@@ -49,7 +49,7 @@ def test_ragged_counts_match_oracle(gpu, N, M, ch, eq, snr, S):
     eng, h, cp = make(N, M, ch, eq)
     seed = 31
     y = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
-    stats = torch.zeros(3, dtype=torch.float64, device="cuda")
+    stats = new_stats("cuda")
     eng.tx(eng.stream(), None, seed, 0, S, y, stats)
     torch.cuda.synchronize()
     ref_y = P.run_philox(seed, S, N, M, h, cp, eq, snr, noise_on=False)
@@ -70,9 +70,9 @@ def test_ragged_offsets_tile_the_run(gpu, N, M, ch, eq, snr):
     eng, _, _ = make(N, M, ch, eq)
     S, seed = 101, 4
     whole = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
-    eng.tx(eng.stream(), None, seed, 0, S, whole, torch.zeros(3, dtype=torch.float64, device="cuda"))
+    eng.tx(eng.stream(), None, seed, 0, S, whole, new_stats("cuda"))
     parts = torch.empty_like(whole)
-    st = torch.zeros(3, dtype=torch.float64, device="cuda")
+    st = new_stats("cuda")
     cuts = [0, 1, 6, 23, 40, 57, 100, S]
     for a, b in zip(cuts[:-1], cuts[1:]):
         eng.tx(eng.stream(), None, seed, a, b - a, parts[a:b], st)

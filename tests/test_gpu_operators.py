@@ -170,3 +170,54 @@ def test_adaptive_mapper_vs_oracle(gpu):
                 rb += [(i >> (b - 1 - j)) & 1 for j in range(b)]
     rb = np.array(rb[: len(rb) // 8 * 8], np.uint8)
     assert out == np.packbits(rb).tobytes()
+
+
+@pytest.mark.parametrize("precision", [B.OFDM_F64, B.OFDM_F32])
+@pytest.mark.parametrize("st", load_stages(), ids=lambda s: s["name"])
+def test_demap_count_matches_reference_counts(gpu, st, precision):
+    """ofdm_demap_count (fused decode + XOR/popcount) on the reference's own equalised symbols Z
+    gives the reference's bit_errors / symbol_errors (constellation/models.py:251-295,
+    simulation/models.py:596-606); complex64: Z rounded to float32, same decisions here."""
+    a = stage_arrays(st["name"])
+    N, M = st["N"], st["M"]
+    plan = B.Plan(n_fft=N, precision=precision, luts=[O.qam_lut(M)])
+    Z = torch.from_numpy(a["Z"]).to(plan.cdtype).to(gpu)
+    tx = torch.from_numpy(a["tx_bytes"].copy()).to(gpu)
+    cnt = torch.zeros(2, dtype=torch.int64, device=gpu)
+    B.check(B.lib().ofdm_demap_count(plan.handle, B.stream_ptr(), B.ptr(Z), B.ptr(tx), Z.shape[0], B.ptr(cnt)))
+    assert tuple(cnt.cpu().tolist()) == (st["bit_errors"], st["symbol_errors"])
+
+
+def test_demap_count_adaptive_vs_oracle(gpu):
+    """CAPACITY_BASED decode + count: per-subcarrier orders, unused subcarriers, the trailing
+    partial byte of the run not compared (constellation/adaptive.py:259-263)."""
+    rng = np.random.default_rng(11)
+    N, S = 64, 7
+    orders = rng.choice([0, 4, 16, 64, 256], size=N)
+    orders[0] = 4
+    m = AdaptiveConstellationMapper(orders, QAMConstellationMapper, N)
+    bps = int(m.get_bits_per_subcarrier().sum())
+    data = rng.integers(0, 256, size=(S * bps + 7) // 8, dtype=np.uint8).tobytes()
+    bits = O.bytes_to_bits(data)[: S * bps].reshape(S, bps)
+    offs = np.concatenate([[0], np.cumsum(m.get_bits_per_subcarrier())[:-1]])
+    X = np.zeros((S, N), complex)
+    idx = np.zeros((S, N), np.int64)
+    for k in range(N):
+        if orders[k]:
+            b = int(np.log2(orders[k]))
+            idx[:, k] = bits[:, offs[k]:offs[k] + b] @ (1 << np.arange(b - 1, -1, -1))
+            X[:, k] = O.qam_lut(int(orders[k]))[idx[:, k]]
+    Z = X + 0.06 * (rng.normal(size=X.shape) + 1j * rng.normal(size=X.shape))
+    ridx = np.zeros_like(idx)
+    for k in range(N):
+        if orders[k]:
+            ridx[:, k] = O.nn_demap(Z[:, k], O.qam_lut(int(orders[k])))
+    import philox_streams as P
+    be, se = P.adaptive_counts((ridx ^ idx).astype(np.int64), m.get_bits_per_subcarrier().astype(np.int64), S)
+    luts, sc = m.lut_tables()
+    plan = B.Plan(n_fft=N, precision=B.OFDM_F64, luts=luts, sc_lut=sc)
+    Zd = torch.from_numpy(Z).to(gpu)
+    tx = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(gpu)
+    cnt = torch.zeros(2, dtype=torch.int64, device=gpu)
+    B.check(B.lib().ofdm_demap_count(plan.handle, B.stream_ptr(), B.ptr(Zd), B.ptr(tx), S, B.ptr(cnt)))
+    assert be > 0 and tuple(cnt.cpu().tolist()) == (be, se)

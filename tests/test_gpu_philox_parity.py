@@ -7,10 +7,13 @@ the oracle's (reference-pinned) arithmetic.  Checked here, per configuration:
 * TX: the kept channel samples y of the complex64 kernel vs the oracle's modulate +
   channel on the same bits (relative 1e-4 of the rms sample: float32 IFFT/FIR rounding),
   and the power / PAPR statistics (relative 1e-5);
-* RX: bit and symbol error counts vs the oracle's on the same bits and noise.  The GPU
-  computes in float32 with the hardware transcendentals, the oracle in float64, so a
-  decision can differ only for received points within ~1e-6 of a boundary: the counts
-  must agree to 3 + 0.1 %.
+* RX: bit and symbol error counts vs the oracle's on the same bits and noise, inside the
+  oracle's decision bracket (philox_streams.decision_bracket): the GPU evaluates the noise
+  radius with the float32 hardware log2 / sqrt and its FFTs in its own arithmetic, so a
+  decision may differ from the oracle's only for a received point within the oracle's bound
+  on that deviation (z_error_bound) of a decision boundary; the bracket counts the errors of
+  every such alternative decision.  complex128 kernels: the bracket is usually a single value
+  (lo = hi), i.e. bit-exact counts; complex64: a few counts wide.
 
 Sizes cover both workgroup shapes of the throughput kernels (512 threads at N <= 1024
 without equaliser, 256 otherwise), the multipath FIR, all three equalisers, QPSK to
@@ -27,7 +30,7 @@ import ofdm_oracle as O
 from ofdm_based_systems import _backend as B
 from ofdm_based_systems.constellation.adaptive import AdaptiveConstellationMapper
 from ofdm_based_systems.constellation.models import QAMConstellationMapper
-from ofdm_based_systems.engine import LinkEngine
+from ofdm_based_systems.engine import LinkEngine, new_stats
 
 pytestmark = pytest.mark.gpu
 
@@ -43,6 +46,17 @@ CASES = [
     (2048, 16, "flat_fading", "NONE", 256, 14.0, B.OFDM_F32, {}),
     (32, 16, "flat_fading", "NONE", 8192, 14.0, B.OFDM_F32, {}),
     (1024, 64, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F64, {}),
+    # complex128 throughput kernels (the headline precision): flat TX + no equaliser (config b),
+    # register-window FIR (4 / 8 taps), the run-time-tap FIR (cp > lanes per symbol), N = 64 ..
+    # 4096 (two-level twiddles and two-wave symbols from 2048, preloaded equaliser at 4096)
+    (1024, 64, "flat_fading", "NONE", 512, 20.0, B.OFDM_F64, {}),
+    (256, 16, "Lin-Phoong_P1", "ZF", 1024, 22.0, B.OFDM_F64, {}),
+    (64, 4, "rayleigh_fading", "ZF", 4096, 14.0, B.OFDM_F64, {}),
+    (64, 16, "severe_multipath", "MMSE", 2048, 18.0, B.OFDM_F64, {}),
+    (2048, 16, "flat_fading", "NONE", 256, 14.0, B.OFDM_F64, {}),
+    (4096, 256, "Lin-Phoong_P1", "MMSE", 96, 31.0, B.OFDM_F64, {}),
+    (256, 16, "severe_multipath", "MMSE", 512, 16.0, B.OFDM_F64, {"cp": 2}),
+    (512, 4, "default_multipath", "ZF", 512, 12.0, B.OFDM_F64, {"cp": 0}),
     # SURVEY 8(f) variants on the generic kernel
     (64, 4, "Lin-Phoong_P2", "ZF", 2048, 20.0, B.OFDM_F32, {"modulator": "SC"}),
     (1024, 16, "severe_multipath", "MMSE", 256, 21.0, B.OFDM_F32, {"prefix": "ZP"}),
@@ -116,7 +130,7 @@ def test_tx_samples_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
     eng, h, cp, var = setup(N, M, ch, eq, prec, var, snr)
     seed = 1234
     y = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
-    stats = torch.zeros(3, dtype=torch.float64, device="cuda")
+    stats = new_stats("cuda")
     eng.tx(eng.stream(), None, seed, 0, S, y, stats)
     torch.cuda.synchronize()
     ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, noise_on=False, **var)
@@ -137,11 +151,13 @@ def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
     eng, h, cp, var = setup(N, M, ch, eq, prec, var, snr)
     seed = 77
     res = eng.run(S, snr, seed=seed)
-    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, **var)
+    ref = P.run_philox(seed, S, N, M, h, cp, eq, snr, precision="f32" if prec == B.OFDM_F32 else "f64", **var)
     assert ref.bit_errors > 100, "SNR too high for a meaningful count"
-    for got, want in ((res.bit_errors, ref.bit_errors), (res.symbol_errors, ref.symbol_errors)):
-        assert abs(got - want) <= 3 + 1e-3 * want, (got, want)
-    assert res.power_sum == pytest.approx(ref.power_sum, rel=1e-5)
+    be_lo, be_hi, se_lo, se_hi = ref.bracket
+    assert be_lo <= ref.bit_errors <= be_hi and se_lo <= ref.symbol_errors <= se_hi
+    assert be_lo <= res.bit_errors <= be_hi, (res.bit_errors, ref.bracket)
+    assert se_lo <= res.symbol_errors <= se_hi, (res.symbol_errors, ref.bracket)
+    assert res.power_sum == pytest.approx(ref.power_sum, rel=1e-5 if prec == B.OFDM_F32 else 1e-12)
 
 
 def test_sharded_halves_add_up_to_the_whole(gpu):
@@ -150,11 +166,11 @@ def test_sharded_halves_add_up_to_the_whole(gpu):
     S = 600
     whole = eng.run(S, 24.0, seed=9)
     y = torch.empty((S, 1024), dtype=eng.cdtype, device="cuda")
-    st = torch.zeros(3, dtype=torch.float64, device="cuda")
+    st = new_stats("cuda")
     eng.tx(eng.stream(), None, 9, 0, 250, y[:250], st)
     eng.tx(eng.stream(), None, 9, 250, S - 250, y[250:], st)
     y2 = torch.empty_like(y)
-    eng.tx(eng.stream(), None, 9, 0, S, y2, torch.zeros(3, dtype=torch.float64, device="cuda"))
+    eng.tx(eng.stream(), None, 9, 0, S, y2, new_stats("cuda"))
     torch.cuda.synchronize()
     assert torch.equal(y, y2)
     assert whole.bit_errors > 0

@@ -4,6 +4,10 @@ Each variant sets OFDM_ABLATE_TX / OFDM_ABLATE_RX (bit flags, see ofdm_launch.hp
 times ofdm_tx / ofdm_rx with HIP events on the launch stream.
 
     python tools/ablate.py [--config b|c|e] [--symbols 1000000]
+
+The switches exist only in the ablation build of the library:
+    make -C ofdm-based-systems_amd VARIANT=ablate EXTRA=-DOFDM_ABLATION=1
+which this script selects (OFDM_LIB_VARIANT=ablate); the product library ignores them.
 """
 
 import argparse
@@ -14,6 +18,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ofdm-based-systems_amd"))
 sys.path.insert(0, ROOT)
+
+os.environ.setdefault("OFDM_LIB_VARIANT", "ablate")  # before the library loads
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
