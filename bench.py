@@ -1,26 +1,33 @@
 """Headline benchmark: OFDM symbols/s through the fused GPU modem path.
 
-Metric (BASELINE.json): OFDM symbols/sec at N_FFT=1024, 64-QAM.  Workload =
-BASELINE config (b): N_FFT=1024, 64-QAM, flat channel (flat_fading.npy, cp=0),
-no equaliser, AWGN at 24 dB (BER ~1e-4), complex64 arithmetic, Philox bits and
-noise generated on the device.  One step = one complete Simulation-run of the hot
-path over `--symbols` OFDM symbols per GPU (TX kernel, power all-reduce, RX
-kernel, counter all-reduce, results on the host).  Default 10 steps x 1e6
-symbols = the "1e7 symbols at one SNR" of config (b).  After the timed region rank 0
-also reports the BER Delta dB of the run against the reference-stream path (the second
-half of the BASELINE metric).
+Metric (BASELINE.json): OFDM symbols/sec at N_FFT=1024, 64-QAM.  Workload = BASELINE config
+(b): N_FFT=1024, 64-QAM, flat channel (flat_fading.npy, cp=0), no equaliser, AWGN at 24 dB
+(BER ~1e-4), Philox bits and noise generated on the device, in complex128 -- the reference's
+arithmetic (np.fft / np.convolve on complex128, modulation/models.py:32,46-48).  One step = one
+complete Simulation-run of the hot path over `--symbols` OFDM symbols per GPU (TX kernel, power
+exchange, RX kernel, counter reduction, counts on the host).  Default 10 steps x 1e6 symbols =
+the "1e7 symbols at one SNR" of config (b).  `value` is measured after exactly `--warmup`
+untimed steps; the same path in complex64 is reported beside it (`c64_variant`), and so is a
+second complex128 measurement after a clock-ramp warmup (`value_after_ramp`).  Rank 0 also
+reports the BER Delta dB of the timed run against the reference-stream path (the second half of
+the BASELINE metric) and the CPU baseline.
 
-Multi-GPU (torchrun): each rank simulates its contiguous share of the global
-symbol range of every step (weak scaling); exchanges: one all-reduce of the
-AWGN power statistics and one of the error counters per step (RCCL).
+Multi-GPU: `--gpus N` without a torch.distributed environment re-launches this script as N
+ranks (torch.distributed.run, one process per GPU, before anything touches a GPU); each rank
+simulates its contiguous share of every step's global symbol range with a fixed share per GPU
+(weak scaling); the exchanges are one all-gather of the 40-byte ofdm_stats record (exact
+fixed-point power) and one all-reduce of the error counters per step (RCCL).
 """
 
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -41,9 +48,12 @@ CONFIGS = {
     "d": (2048, 0, "Lin-Phoong_P1", 1.0, "MMSE", 20.0,
           "config (d): N_FFT=2048, adaptive bit loading (water-filling, desired SER 1e-3), Lin-Phoong_P1.npy "
           "(4 taps, cp=3), MMSE, AWGN 20 dB"),
-    "e": (4096, 256, "Lin-Phoong_P1", 1.0, "MMSE", 30.0,
-          "config (e): N_FFT=4096, 256-QAM, Lin-Phoong_P1.npy (4 taps, cp=3), MMSE, AWGN 30 dB"),
+    # 38.75 dB: the BER 1e-4 crossing of this config (profiles/r02g_ber_curve_e.json: 38.67 dB)
+    "e": (4096, 256, "Lin-Phoong_P1", 1.0, "MMSE", 38.75,
+          "config (e): N_FFT=4096, 256-QAM, Lin-Phoong_P1.npy (4 taps, cp=3), MMSE, AWGN 38.75 dB"),
 }
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PRECISIONS = {"f64": ("c128 (f64)", 16), "f32": ("c64 (f32)", 8)}
 
 
 def make_engine(cfg, precision):
@@ -69,16 +79,35 @@ def make_engine(cfg, precision):
         luts, sc = AdaptiveConstellationMapper(orders, QAMConstellationMapper, N).lut_tables()
     else:
         luts = [QAMConstellationMapper(M).constellation]
-    return LinkEngine(N, cp, h, eq, luts, sc, precision), h, cp
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+    prec = B.OFDM_F32 if precision == "f32" else B.OFDM_F64
+    return LinkEngine(N, cp, h, eq, luts, sc, prec)
 
 
-def kernel_bytes_per_symbol(N: int, bps: int, cp: int) -> int:
+def kernel_bytes_per_symbol(N: int, bps: int, cp: int, w: int = 8) -> int:
     """Algorithmic bytes one OFDM symbol moves in ONE of the two kernels:
-    B_alg = 2*ceil(bps/8) + 2*(N+cp)*8 per symbol (bps = N*b, or sum b_k with adaptive loading)
-    is split evenly: each kernel touches the tx bits once (map / comparator) and the complex64
-    channel stream once (write / read)."""
-    return math.ceil(bps / 8) + (N + cp) * 8
+    B_alg = 2*ceil(bps/8) + 2*(N+cp)*w per symbol (bps = N*b, or sum b_k with adaptive loading;
+    w = 16 bytes per complex128 sample, 8 per complex64) is split evenly: each kernel touches the
+    tx bits once (map / comparator) and the channel stream once (write / read)."""
+    return math.ceil(bps / 8) + (N + cp) * w
+
+
+# ---------------------------------------------------------------------------- CPU baseline
+def host_cores() -> int:
+    """CPUs this process may use: its affinity set, capped by the cgroup CPU quota when one is
+    set (on the GPU box os.cpu_count() and the affinity set report every CPU of the machine,
+    while the job's share is a quota)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def _cpu_worker(args):
@@ -87,29 +116,30 @@ def _cpu_worker(args):
 
     seed, S, N, M, ch, cp, eq, snr = args
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
+    t0 = time.perf_counter()  # stream generation included, as the GPU leg generates its streams
     if M == 0:  # CAPACITY_BASED: orders from water-filling, the adaptive data path
         orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
         bps = int(sum(int(np.log2(o)) for o in orders if o > 0))
         tx, nz = O.reference_streams(seed, S * bps, S * (N + cp))
-        t0 = time.perf_counter()
         O.run_adaptive(tx, orders, N, h, cp, eq, snr, nz)
-        return S, time.perf_counter() - t0
-    b = int(np.log2(M))
-    tx, nz = O.reference_streams(seed, S * N * b, S * (N + cp))
-    t0 = time.perf_counter()
-    O.run_fixed(tx, S * N * b, N, M, h, cp, eq, snr, nz)
+    else:
+        b = int(np.log2(M))
+        tx, nz = O.reference_streams(seed, S * N * b, S * (N + cp))
+        O.run_fixed(tx, S * N * b, N, M, h, cp, eq, snr, nz)
     return S, time.perf_counter() - t0
 
 
 def cpu_baseline(cfg, per_worker: int):
-    """The NumPy oracle (a port of the reference path) on the host cores, bounded sample."""
+    """The NumPy oracle (a port of the reference path, complex128 like the reference) on every
+    CPU of this process, one worker per core, bounded sample."""
     import multiprocessing as mp
 
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     N, M, ch, ratio, eq, snr, _ = cfg
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
     cp = int(ratio * (len(h) - 1))
-    workers = max(1, min(16, os.cpu_count() or 1))
+    if M == 0:  # whole-byte runs: the adaptive decode needs S * sum(b_k) % 8 == 0
+        per_worker = 8 * math.ceil(per_worker / 8)
+    workers = host_cores()
     jobs = [(100 + i, per_worker, N, M, ch, cp, eq, snr) for i in range(workers)]
     ctx = mp.get_context("spawn")
     t0 = time.perf_counter()
@@ -120,13 +150,16 @@ def cpu_baseline(cfg, per_worker: int):
     cpu_s = sum(o[1] for o in out)
     return {
         "value": syms / wall, "unit": "OFDM symbols/s", "cores": workers, "kind": "port",
-        "sample": f"{workers} processes x {per_worker} OFDM symbols of the same config through the NumPy "
-                  f"oracle (reference PCG64 bits + legacy-normal noise; stream generation untimed), "
+        "host_cpu_count": os.cpu_count(),
+        "sample": f"{workers} processes (one per CPU of this process's affinity set; the machine reports "
+                  f"{os.cpu_count()}) x {per_worker} OFDM symbols of the same config through the NumPy oracle in "
+                  f"complex128, reference PCG64 bits + legacy-normal noise generated inside the timing; "
                   f"{cpu_s:.1f} s of CPU work, {wall:.1f} s wall incl. process start",
         "per_core_symbols_per_s": syms / cpu_s,
     }
 
 
+# ---------------------------------------------------------------------------- accuracy check
 def ber_vs_reference(engine64, N, cp, snr, ber_phx, bits_phx, symbols=16000, seed=1):
     """BER Delta dB of the timed throughput run against the reference-stream path at the same SNR.
 
@@ -156,18 +189,180 @@ def ber_vs_reference(engine64, N, cp, snr, ber_phx, bits_phx, symbols=16000, see
             "delta_db": delta, "delta_db_stderr": sd_db, "bar_db": 0.05}
 
 
-def pmc_traffic(config_name: str, symbols_per_launch: int):
-    """HBM bytes per launch of the dominant kernel from a committed rocprofv3 --pmc summary
+def pmc_traffic(key: str, symbols_per_launch: int):
+    """HBM bytes per launch of each kernel from a committed rocprofv3 --pmc summary
     (profiles/pmc_summary.json, produced by tools/pmc_summary.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         pm = json.load(f)
-    rec = pm.get(config_name)
+    rec = pm.get(key)
     if not rec:
         return None
     return {k: v * symbols_per_launch / rec["symbols_per_launch"] for k, v in rec["bytes_per_launch"].items()}
+
+
+# ---------------------------------------------------------------------------- ranks
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc: int) -> int:
+    """Run this script as `nproc` ranks under torch.distributed.run (a child process started
+    before anything here touches a GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+class Runtime:
+    """Device, stream-synchronisation and collective helpers for one rank (GPU, or the CPU when
+    a test engine factory runs the bench without a GPU)."""
+
+    def __init__(self, backend: str, cpu: bool):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.cpu = cpu
+        self.group = None
+        # OFDM_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a 1-GPU box
+        # (with --backend gloo; RCCL refuses two ranks on one GPU)
+        self.dev = int(os.environ.get("OFDM_BENCH_DEVICE", self.local))
+        if not cpu:
+            torch.cuda.set_device(self.dev)
+        if self.world > 1:
+            import torch.distributed as dist
+
+            if backend == "nccl" and not cpu:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.dev))
+            else:
+                dist.init_process_group(backend)
+            self.group = dist.group.WORLD
+            self.world = dist.get_world_size()
+
+    def sync(self):
+        if not self.cpu:
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    def max_over_ranks(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch.distributed as dist
+
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if self.cpu else "cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj):
+        if self.world == 1:
+            return [obj]
+        import torch.distributed as dist
+
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
+
+    def finish(self):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+            dist.destroy_process_group()
+
+
+def timed_steps(rt: Runtime, engine, total: int, snr: float, steps: int, seed0: int, events):
+    """K complete runs (one per step), enqueued as LinkEngine.run_pipelined schedules them and
+    read back inside the timed region, bracketed by barrier + device synchronisation; the
+    elapsed time is the maximum over ranks."""
+    rt.sync()
+    rt.barrier()
+    rt.sync()
+    t0 = time.perf_counter()
+    pending = engine.run_pipelined(total, snr, range(seed0, seed0 + steps), group=rt.group, events=events)
+    bit_errors = sum(p.result().bit_errors for p in pending)
+    rt.sync()
+    rt.barrier()
+    rt.sync()
+    return rt.max_over_ranks(time.perf_counter() - t0), bit_errors
+
+
+def roofline(events, N: int, bps: int, cp: int, w: int, traffic):
+    """The dominant kernel's algorithmic bytes per launch over its average launch time (HIP
+    events recorded on the launch stream around every ofdm_tx / ofdm_rx)."""
+    if not events:
+        return None
+    durs = {}
+    for name, n, e0, e1 in events:
+        durs.setdefault(name, []).append((e0.elapsed_time(e1) * 1e-3, n))
+    avg = {k: sum(d for d, _ in v) / len(v) for k, v in durs.items()}
+    dom = max(avg, key=avg.get)
+    per_launch = durs[dom][0][1]
+    alg = kernel_bytes_per_symbol(N, bps, cp, w)
+    achieved = alg * per_launch / avg[dom] / 1e9
+    return {
+        "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS,
+        "traffic": None if traffic is None else traffic.get(dom),
+        "alg_bytes_per_symbol": alg, "symbols_per_launch": per_launch,
+        "avg_launch_ms": {k: v * 1e3 for k, v in avg.items()},
+    }
+
+
+def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp: bool):
+    """W untimed warmup steps, then K timed steps; optionally a clock-ramp warmup and K more
+    timed steps (value_after_ramp)."""
+    N, M, ch, ratio, eq_name, snr, _ = cfg
+    engine = factory(cfg, precision)
+    cp, bps = engine.cp, engine.bps
+    total = per_gpu * rt.world
+    # the two runs' channel-sample buffers the pipelined schedule keeps alive, allocated before
+    # the warmup (a first-time hipMalloc of 2 x 16.4 GB would otherwise land in the timed steps)
+    engine.reserve(total, 2, group=rt.group)
+    for i in range(args.warmup):
+        engine.run(total, snr, seed=10_000 + i, group=rt.group)
+    events = None if rt.cpu else []
+    elapsed, bit_errors = timed_steps(rt, engine, total, snr, args.steps, 0, events)
+    w = PRECISIONS[precision][1]
+    key = args.config if precision == "f32" else f"{args.config}_{precision}"
+    rec = {
+        "value": total * args.steps / elapsed,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "dtype": PRECISIONS[precision][0],
+        "roofline": roofline(events, N, bps, cp, w, None if rt.cpu else pmc_traffic(key, per_gpu)),
+        "ber": bit_errors / (engine.valid_bits(total) * args.steps),
+        "bits": engine.valid_bits(total) * args.steps,
+    }
+    rec["path_hbm_fraction"] = rec["value"] * 2 * kernel_bytes_per_symbol(N, bps, cp, w) / (
+        HBM_PEAK_GBS * 1e9 * rt.world)
+    if ramp and args.ramp_seconds > 0:
+        # a fresh box idles at low clocks and needs ~40 ms of load to reach the steady state its
+        # power cap sets (profiles/r02_ramp_b.json): keep running untimed steps for --ramp-seconds,
+        # then time K more
+        extra, t_ramp = 0, time.perf_counter()
+        while True:
+            done = torch.tensor([time.perf_counter() - t_ramp >= args.ramp_seconds], dtype=torch.int32,
+                                device="cpu" if rt.cpu else "cuda")
+            if rt.world > 1:
+                import torch.distributed as dist
+
+                dist.all_reduce(done, op=dist.ReduceOp.MIN)  # every rank runs the same number of steps
+            if int(done.item()):
+                break
+            engine.run(total, snr, seed=20_000 + extra, group=rt.group)
+            extra += 1
+        e2, _ = timed_steps(rt, engine, total, snr, args.steps, 30_000, None)
+        rec["value_after_ramp"] = {"value": total * args.steps / e2, "ms_per_step": e2 / args.steps * 1e3,
+                                   "extra_untimed_steps": extra, "ramp_seconds": args.ramp_seconds}
+    return engine, rec
 
 
 def main():
@@ -176,153 +371,83 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--symbols", type=int, default=0,
-                    help="OFDM symbols per GPU per step (default 1e6 x 1024/N: 8.2 GB of channel samples)")
+                    help="OFDM symbols per GPU per step (default 1e6 x 1024/N)")
     ap.add_argument("--config", default="b", choices=sorted(CONFIGS))
-    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--precision", default="f64", choices=sorted(PRECISIONS),
+                    help="arithmetic of the headline line (f64 = complex128, the reference's)")
+    ap.add_argument("--no-variant", action="store_true", help="skip the complex64 companion run")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="OFDM symbols per CPU worker (default 1500 x 1024/N)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ber-check", action="store_true", help="skip the BER Delta-dB check vs the reference streams")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--ramp-seconds", type=float, default=0.25,
-                    help="untimed warmup beyond --warmup until this much GPU time has passed (clock ramp)")
+                    help="clock-ramp warmup before the value_after_ramp measurement (0: skip it)")
+    ap.add_argument("--engine-factory", default=None, help=argparse.SUPPRESS)  # tests: module:function
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # OFDM_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a 1-GPU box
-    # (with --backend gloo; RCCL refuses two ranks on one GPU)
-    dev = int(os.environ.get("OFDM_BENCH_DEVICE", local))
-    torch.cuda.set_device(dev)
-    group = None
-    if world > 1:
-        import torch.distributed as dist
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(args.backend)
-        group = dist.group.WORLD
-
-    from ofdm_based_systems import _backend as B
+    factory = make_engine
+    if args.engine_factory:
+        mod, fn = args.engine_factory.split(":")
+        factory = getattr(importlib.import_module(mod), fn)
+    rt = Runtime(args.backend, cpu=bool(args.engine_factory) and not torch.cuda.is_available())
+    if args.gpus > 1 and rt.world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={rt.world}")
 
     cfg = CONFIGS[args.config]
     N, M, ch, ratio, eq_name, snr, desc = cfg
-    prec = B.OFDM_F32 if args.precision == "f32" else B.OFDM_F64
-    engine, h, cp = make_engine(cfg, prec)
-    bps = engine.bps  # bits per OFDM symbol
     per_gpu = args.symbols if args.symbols else 1_000_000 // max(1, N // 1024)
-    total = per_gpu * world
+    total = per_gpu * rt.world
+    engine, head = measure(rt, args, cfg, args.precision, per_gpu, factory, ramp=True)
+    variant = None
+    if not args.no_variant:
+        other = "f32" if args.precision == "f64" else "f64"
+        _, variant = measure(rt, args, cfg, other, per_gpu, factory, ramp=False)
+    devices = rt.gather(rt.dev if not rt.cpu else "cpu")
 
-    def barrier():
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.barrier()
-
-    for i in range(args.warmup):
-        engine.run(total, snr, seed=10_000 + i, group=group)
-    torch.cuda.synchronize()
-    # Clock ramp: a fresh box idles at ~100-350 MHz and its clock needs ~40 ms of load to reach
-    # the steady state the power cap sets (tools/ramp_probe.py, profiles/r02_ramp_b.json), longer
-    # than a few warmup steps.  Keep warming up (untimed, outside the K timed steps) until
-    # --ramp-seconds of GPU work have run; the extra steps are reported.
-    ramp_steps, t_ramp = 0, time.perf_counter()
-    while args.ramp_seconds > 0:
-        done = torch.tensor([time.perf_counter() - t_ramp >= args.ramp_seconds], dtype=torch.int32, device="cuda")
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.all_reduce(done, op=dist.ReduceOp.MIN)  # every rank runs the same number of steps
-        if int(done.item()):
-            break
-        engine.run(total, snr, seed=20_000 + ramp_steps, group=group)
-        ramp_steps += 1
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    events = []
-    bit_errors = 0
-    t0 = time.perf_counter()
-    # every step is the whole hot path (bits -> ... -> error counts) of one run; the host
-    # enqueues all steps (step k+1's TX ahead of step k's RX, so the ranks' statistics
-    # exchange overlaps a transmitter) and reads every run's counts back inside the timed region
-    pending = engine.run_pipelined(total, snr, range(args.steps), group=group, events=events)
-    for p in pending:
-        bit_errors += p.result().bit_errors
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        import torch.distributed as dist
-
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # per-kernel average launch duration from HIP events on the launch stream
-    durs = {}
-    for name, n, e0, e1 in events:
-        durs.setdefault(name, []).append((e0.elapsed_time(e1) * 1e-3, n))
-    avg = {k: sum(d for d, _ in v) / len(v) for k, v in durs.items()}
-    dom = max(avg, key=avg.get)
-    sym_per_launch = durs[dom][0][1]
-    alg = kernel_bytes_per_symbol(N, bps, cp) * sym_per_launch
-    achieved = alg / avg[dom] / 1e9
-    traffic = pmc_traffic(args.config, sym_per_launch)
-    value = total * args.steps / elapsed
     out = {
         "metric": "OFDM symbols/sec (1/2/4/8 GPU) at N_FFT=1024 64-QAM; BER ΔdB vs ref",
-        "value": value,
+        "value": head["value"],
         "unit": "OFDM symbols/s",
-        "n_gpus": world,
+        "n_gpus": rt.world,
+        "devices": devices,
         "steps": args.steps,
         "warmup": args.warmup,
-        "clock_ramp": {"extra_untimed_steps": ramp_steps, "seconds": args.ramp_seconds},
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": head["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "c64 (f32)" if prec == B.OFDM_F32 else "c128 (f64)",
+        "dtype": head["dtype"],
         "data": "synthetic: Philox4x32-10 / MWC64X bits and Box-Muller AWGN (64-point phase table) generated "
-                "on the GPU per (seed, symbol)",
+                "on the GPU per (seed, symbol); noise radius exact to 5.65 sigma (BER curves valid down to "
+                "~1e-7)",
         "config": {
             "workload": f"{desc}; {per_gpu} OFDM symbols per GPU per step",
-            "n_fft": N, "qam_order": M if M else "adaptive", "bits_per_ofdm_symbol": bps, "cp": cp,
+            "n_fft": N, "qam_order": M if M else "adaptive", "bits_per_ofdm_symbol": engine.bps, "cp": engine.cp,
             "channel": ch, "equalizer": eq_name, "snr_db": snr,
-            "symbols_per_step": total, "parallelism": f"symbol-sharded x{world}",
+            "symbols_per_step": total, "parallelism": f"symbol-sharded x{rt.world}",
         },
-        "roofline": {
-            "bound": "hbm",
-            "kernel": dom,
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None if traffic is None else traffic.get(dom),
-            "alg_bytes_per_symbol": kernel_bytes_per_symbol(N, bps, cp),
-            "symbols_per_launch": sym_per_launch,
-            "avg_launch_ms": {k: v * 1e3 for k, v in avg.items()},
-        },
-        "path_hbm_fraction": value * 2 * kernel_bytes_per_symbol(N, bps, cp) / (HBM_PEAK_GBS * 1e9 * world),
-        "ber": bit_errors / (engine.valid_bits(total) * args.steps),
+        "roofline": head["roofline"],
+        "path_hbm_fraction": head["path_hbm_fraction"],
+        "ber": head["ber"],
     }
-    if rank == 0 and not args.no_ber_check:
-        eng64, _, _ = make_engine(cfg, B.OFDM_F64)
-        out["ber_vs_reference"] = ber_vs_reference(eng64, N, cp, snr, out["ber"],
-                                                   engine.valid_bits(total) * args.steps,
+    if "value_after_ramp" in head:
+        out["value_after_ramp"] = head["value_after_ramp"]
+    if variant is not None:
+        out[("c64" if variant["dtype"].startswith("c64") else "c128") + "_variant"] = {
+            k: variant[k] for k in ("value", "ms_per_step", "dtype", "roofline", "path_hbm_fraction", "ber")}
+    if rt.rank == 0 and not args.no_ber_check and not rt.cpu:
+        eng64 = make_engine(cfg, "f64")
+        out["ber_vs_reference"] = ber_vs_reference(eng64, N, engine.cp, snr, head["ber"], head["bits"],
                                                    symbols=max(2000, 16000 * 1024 // N))
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rt.rank == 0 and rt.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or max(100, 1500 * 1024 // N))
-    if rank == 0:
+    if rt.rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.barrier()
-        dist.destroy_process_group()
+    rt.finish()
 
 
 if __name__ == "__main__":

@@ -59,6 +59,7 @@ __device__ __forceinline__ R norm2(cpx<R> a) { return a.re * a.re + a.im * a.im;
 // components in one issue slot (the f32 vector peak of CDNA4 is only reached packed);
 // swizzles and negations fold into the op_sel / neg_lo / neg_hi operand modifiers.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
 template <>
 struct cpx<float> {
     union {
@@ -1024,6 +1025,13 @@ constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2)
 // carry into the addend pair and the xor) per 32-bit output.  Seeded from one Philox block:
 // c = (P1 >> 1) | 1 < A, so the state is never one of the two fixed points.
 constexpr uint32_t kMwcA = 4294883355u;
+// sqrt(32 - log2(float(w | 0x1F8))) on the float32 hardware log2 / sqrt.  The |.| (a free source
+// modifier) keeps the square root real when the approximate log2 of a word rounding to 2^32
+// comes out slightly above 32: the radius is then ~0 instead of NaN.
+__device__ __forceinline__ float noise_radius(uint32_t w) {
+    return __builtin_amdgcn_sqrtf(__builtin_fabsf(32.0f - __builtin_amdgcn_logf((float)(w | kNoisePhaseMask))));
+}
+
 struct Mwc64x {
     uint32_t x, c;
     __device__ __forceinline__ void seed(uint32_t p0, uint32_t p1) {
@@ -1044,7 +1052,7 @@ struct Mwc64x {
     // holding sigma sqrt(2 ln 2)).  Bits 3..8 are forced to 1 in the radius word, so radius and
     // phase come from disjoint bits.
     __device__ __forceinline__ static f32x2 sample(uint32_t w, const f32x2* ntab, float& r) {
-        r = __builtin_amdgcn_sqrtf(32.0f - __builtin_amdgcn_logf((float)(w | kNoisePhaseMask)));
+        r = noise_radius(w);
         return *(const f32x2*)((const unsigned char*)ntab + (w & kNoisePhaseMask));
     }
     __device__ __forceinline__ void add_noise(f32x2& x0, const f32x2* ntab) {
@@ -1057,14 +1065,29 @@ struct Mwc64x {
         const f32x2 e = sample(next(), ntab, r);
         return f32x2{r, r} * e;
     }
+    // complex128 kernels: the same radius and phase entry, the product taken in double against
+    // ntab64 = the float32 table entries widened (exact), fused into the sample: one conversion
+    // and two v_fma_f64 instead of a float product and two conversions.  Bits 3..8 of w address
+    // the 16-byte entries as (w & 0x1F8) * 2.
+    __device__ __forceinline__ void add_noise64(double& re, double& im, const f64x2* ntab64) {
+        const uint32_t w = next();
+        const float r = noise_radius(w);
+        const f64x2 e = *(const f64x2*)((const unsigned char*)ntab64 + 2 * (w & kNoisePhaseMask));
+        const double rd = (double)r;
+        re = __builtin_fma(rd, e.x, re);
+        im = __builtin_fma(rd, e.y, im);
+    }
 };
 
-// Build the noise phase table in LDS (threads < 64; caller syncs).
-__device__ __forceinline__ void build_noise_table(f32x2* ntab, double sigma) {
+// Build the noise phase table in LDS (threads < 64; caller syncs); ntab64 (complex128 kernels,
+// or null): the same float32 entries widened to double.
+__device__ __forceinline__ void build_noise_table(f32x2* ntab, double sigma, f64x2* ntab64 = nullptr) {
     if (threadIdx.x < kNoisePhases) {
         const float s = (float)(sigma * kSqrt2Ln2);
         const double th = (2.0 * threadIdx.x + 1.0) / kNoisePhases;  // (j + 1/2) / 32 half-turns
-        ntab[threadIdx.x] = f32x2{s * (float)cospi(th), s * (float)sinpi(th)};
+        const f32x2 e = f32x2{s * (float)cospi(th), s * (float)sinpi(th)};
+        ntab[threadIdx.x] = e;
+        if (ntab64) ntab64[threadIdx.x] = f64x2{(double)e.x, (double)e.y};
     }
 }
 

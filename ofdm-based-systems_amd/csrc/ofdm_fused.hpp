@@ -65,8 +65,6 @@
 
 namespace ofdm {
 
-typedef double f64x2 __attribute__((ext_vector_type(2)));
-
 template <bool NT, typename C>
 __device__ __forceinline__ C ld_stream(const C* p) {
     if constexpr (NT && sizeof(C) == 8) {
@@ -383,11 +381,14 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     const bool adaptive = FB ? false : (bool)cm.adaptive;
     // generic kernel variants: single-carrier OFDM (no IFFT, modulation/models.py:
     // 58-70) and the zero-padding guard (prefix/models.py:55-67: [x | 0 ... 0])
-    const bool scm = FB == 1 ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
+    // (the complex128 throughput kernels take OFDM with a cyclic prefix only: the launcher sends
+    // SC-OFDM and zero padding to the generic kernel, so both are compiled out of them)
+    constexpr bool F64_FAST = sizeof(R) == 8 && FB > 0;
+    const bool scm = (FB == 1 || F64_FAST) ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
     // zero-padding guard (run-time, uniform); compiled out of the flat throughput TX (a zero
     // guard needs cp > 0, the launcher sends it to the LT = -1 kernel), where the run-time
     // row stride alone cost 15 % (config b TX 1.64 -> 1.92 ms)
-    constexpr bool ZP_OK = !(FB == 1 || (FB > 1 && LT == 0));
+    constexpr bool ZP_OK = !(FB == 1 || (FB > 1 && LT == 0) || F64_FAST);
     const bool zp = ZP_OK ? (bool)cm.zpad : false;
     const int ystride = ZP_OK ? cm.ystride : N;  // stored samples per OFDM symbol: N, or N + cp (ZP)
     const int cp = cm.cp, L = LT != 0 ? a.L : 1;
@@ -753,15 +754,19 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     // generic kernel variants: single-carrier OFDM (FFT -> equalise -> IFFT,
     // modulation/models.py:72-91), zero-padding guard (overlap-add, prefix/models.py:69-101)
     // and non-separable constellations (PSK: brute-force nearest point, constellation/models.py:19-27)
-    const bool scm = FB == 1 ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
-    const bool zp = FB == 1 ? false : (bool)cm.zpad;  // zero-padding guard (run-time, uniform)
+    constexpr bool F64_FAST = sizeof(R) == 8 && FB > 0;  // OFDM + cyclic prefix only (see k_tx)
+    const bool scm = (FB == 1 || F64_FAST) ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
+    const bool zp = (FB == 1 || F64_FAST) ? false : (bool)cm.zpad;  // zero-padding guard (run-time, uniform)
     const bool nn = FB ? false : (bool)cm.nn;
-    const int ystride = FB == 1 ? N : cm.ystride;
+    const int ystride = (FB == 1 || F64_FAST) ? N : cm.ystride;
     // odd bits per subcarrier (FB = 3, 5): the reference's 8- / 32-PSK only
     constexpr bool FB_PSK_ONLY = FB > 1 && (FB & 1);
     // noise phase table: static LDS at a link-time constant address, so a lane word's bits 3..8
     // (its byte offset) address an entry with no add
     __shared__ f32x2 ntab[kNoisePhases];
+    // complex128 throughput kernels: the table widened to double (Mwc64x::add_noise64)
+    __shared__ f64x2 ntab64_s[F64_FAST ? kNoisePhases : 1];
+    f64x2* ntab64 = F64_FAST ? ntab64_s : nullptr;
     Carve cv(ofdm_smem);
     constexpr bool TT = uses_tt<R, LOGN, FB>();
     constexpr bool SPLIT = split_rows<R, FB>();  // complex128 throughput: rows of reals
@@ -795,7 +800,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
         sigma_d = sqrt((p / a.snr_lin) / 2.0);
     }
     const R sigma = (R)sigma_d;
-    build_noise_table(ntab, sigma_d);
+    build_noise_table(ntab, sigma_d, ntab64);
     if constexpr (!TT) load_twiddles<R>(tw, (const C*)cm.tw);
     for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
     if constexpr (EQ_LDS)
@@ -927,6 +932,8 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
             for (int i = 0; i < E; ++i) {
                 if constexpr (sizeof(R) == 4) {
                     tb.g.add_noise(x[i].v, ntab);
+                } else if constexpr (F64_FAST) {
+                    tb.g.add_noise64(x[i].re, x[i].im, ntab64);
                 } else {
                     const f32x2 n = tb.g.noise(ntab);
                     x[i] = x[i] + mk<R>((R)n.x, (R)n.y);

@@ -143,6 +143,20 @@ class LinkEngine:
                                   int(sym0), int(n_sym), int(n_valid), B.ptr(counters), B.ptr(z_out),
                                   int(z_keep)))
 
+    def reserve(self, n_sym: int, runs_in_flight: int = 2, group=None) -> None:
+        """Allocate, and hand back to torch's caching allocator, the channel-sample buffers of
+        ``runs_in_flight`` concurrent runs of n_sym global symbols (run_pipelined keeps two
+        alive), so that later runs reuse them instead of paying for a multi-GB hipMalloc."""
+        world, rank = 1, 0
+        if group is not None:
+            import torch.distributed as dist
+
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+        lo, hi = shard(n_sym, rank, world)
+        bufs = [torch.empty((max(hi - lo, 1), self.ystride), dtype=self.cdtype, device=self.device())
+                for _ in range(runs_in_flight)]
+        del bufs
+
     # ------------------------------------------------------------------ run
     def run(self, n_sym: int, snr_db: float, **kw) -> LinkStats:
         """Simulate global OFDM symbols [0, n_sym) and return the counts (see :meth:`run_async`)."""

@@ -43,3 +43,27 @@ def test_adaptive_config_orders_follow_the_reference_rule():
     orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
     bps = sum(int(np.log2(o)) for o in orders if o > 0)
     assert 0 < bps < 8 * N and all(o == 0 or (o & (o - 1)) == 0 for o in orders)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` (no torch.distributed environment) launches two ranks itself and
+    reports n_gpus 2 from the process group (gloo, CPU engine double instead of the kernels)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
+                                         os.path.join(ROOT, "ofdm-based-systems_amd"), env.get("PYTHONPATH", "")])
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--engine-factory", "bench_double:make_engine", "--config", "b", "--symbols", "3",
+                        "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-ber-check", "--no-variant",
+                        "--ramp-seconds", "0"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["devices"] == ["cpu", "cpu"]
+    assert d["config"]["symbols_per_step"] == 6 and d["scaling"] == "weak"
+    assert d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0

@@ -85,13 +85,16 @@ def test_phase_table_projection_tails(phi):
 
 def test_radius_words():
     """radius^2 sigma^2 2 ln2 (32 - log2(w | 0x1F8)) = -2 sigma^2 ln u, u = (w | 0x1F8) 2^-32;
-    truncated at u = 504 2^-32 (5.65 sigma), never zero."""
+    truncated at u = 504 2^-32 (5.65 sigma); zero for the words whose float32 rounds to 2^32
+    (w >= 0xFFFFFF80: 2^-25 of the words).  The component tail beyond ~4.5 sigma is depleted
+    by the truncation, so throughput-mode BER is valid down to ~1e-7."""
     w = np.array([0, 0x1F8, 0xFFFFFFFF, 1 << 20], np.uint32)
     n = P.noise_from_words(w, 1.0)
     u = (w | 0x1F8).astype(np.float64) / 2.0 ** 32
     u[2] = 1.0  # float32(0xFFFFFFFF) rounds to 2^32
     assert np.allclose(np.abs(n), np.sqrt(-2 * np.log(u)), rtol=1e-6)
     assert abs(np.abs(n[0]) - 5.6498) < 1e-3
+    assert np.abs(n[2]) == 0.0
 
 
 def test_noise_is_complex_gaussian():

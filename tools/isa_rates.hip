@@ -71,6 +71,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define A_FMAS(v) asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(v) : "s"((float)seed), "v"((float)threadIdx.x))
 #define A_FMAC(v) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(v) : "v"((float)seed), "v"((float)threadIdx.x))
 #define A_CNDS(v) asm volatile("v_cndmask_b32 %0, %0, %1, %2" : "+v"(v) : "v"(seed), "s"((uint64_t)seed))
+#define ID(k) ((double)(threadIdx.x + (k)) * 1e-3 + 0.5)
+#define A_ADDD(v) asm volatile("v_add_f64 %0, %0, %1" : "+v"(v) : "v"((double)seed))
+#define A_MULD(v) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(v) : "v"((double)seed))
+#define A_FMAD(v) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(v) : "v"((double)seed), "v"((double)threadIdx.x))
+#define A_FMACD(v) asm volatile("v_fmac_f64 %0, %1, %2" : "+v"(v) : "v"((double)seed), "v"((double)threadIdx.x))
+#define A_CVTD(v) asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(v) : "v"((float)v))
+#define A_MOVD(v) asm volatile("v_mov_b64 %0, %1" : "=v"(v) : "v"(v + 1.0))
+#define A_RCPD(v) asm volatile("v_rcp_f64 %0, %0" : "+v"(v))
 #define A_CMP(v) asm volatile("v_cmp_gt_u32 vcc, %0, %1\n v_addc_co_u32 %0, vcc, 0, %0, vcc" : "+v"(v) : "v"(seed) : "vcc")
 
 KERNEL(k_add, uint32_t, IU, A_ADD)
@@ -120,6 +128,13 @@ KERNEL(k_pkmul2, f2, IF2, A_PKMUL2)
 KERNEL(k_fmas, float, IF, A_FMAS)
 KERNEL(k_fmac, float, IF, A_FMAC)
 KERNEL(k_cnds, uint32_t, IU, A_CNDS)
+KERNEL(k_addd, double, ID, A_ADDD)
+KERNEL(k_muld, double, ID, A_MULD)
+KERNEL(k_fmad, double, ID, A_FMAD)
+KERNEL(k_fmacd, double, ID, A_FMACD)
+KERNEL(k_cvtd, double, ID, A_CVTD)
+KERNEL(k_movd, double, ID, A_MOVD)
+KERNEL(k_rcpd, double, ID, A_RCPD)
 
 template <typename T>
 static double run(void (*k)(T*, uint32_t), const char* name, double ref_ms) {
@@ -193,5 +208,12 @@ int main() {
     run(k_fmas, "fma(sgpr,2v)", r);
     run(k_fmac, "v_fmac(3v)", r);
     run(k_cnds, "cndmask(sgpr)", r);
+    run(k_addd, "v_add_f64", r);
+    run(k_muld, "v_mul_f64", r);
+    run(k_fmad, "v_fma_f64", r);
+    run(k_fmacd, "v_fmac_f64", r);
+    run(k_cvtd, "v_cvt_f64_f32", r);
+    run(k_movd, "v_mov_b64", r);
+    run(k_rcpd, "v_rcp_f64", r);
     return 0;
 }

@@ -1,6 +1,6 @@
 """Condense a tools/profile.sh run into committed summaries under profiles/.
 
-    python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> <config> <symbols_per_launch>
+    python tools/pmc_summary.py gpurun_out/prof_<tag> <tag> <config> <symbols_per_launch> [f32|f64]
 
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --kernel-trace --stats summary),
 profiles/<tag>_summary.json and merges the per-launch HBM traffic of the two fused
@@ -23,14 +23,19 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+PREC = "f32"
+
+
 def kernel_key(name: str):
-    """The bench's complex64 fused kernels; the complex128 reference-stream launches of the
-    BER check (k_rx<double ...>) are not the timed workload."""
-    if "<float" not in name:
+    """The bench's fused throughput kernels in the profiled precision (k_tx<R, LOGN, FB, LT>,
+    k_rx<R, LOGN, EQ, FB> with FB > 0); the generic kernel's reference-stream launches of the
+    BER check (FB = 0) are not the timed workload."""
+    if ("<float" if PREC == "f32" else "<double") not in name or "<" not in name:
         return None
-    if "k_rx" in name:
+    args = [a.strip() for a in name[name.index("<") + 1:name.index(">")].split(",")]
+    if "k_rx" in name and len(args) == 4 and int(args[3]) > 0:
         return "ofdm_rx"
-    if "k_tx" in name:
+    if "k_tx" in name and len(args) == 4 and int(args[2]) > 0:
         return "ofdm_tx"
     return None
 
@@ -46,7 +51,10 @@ def counters(path, counter):
 
 
 def main():
+    global PREC
     src, tag, config, syms = sys.argv[1], sys.argv[2], sys.argv[3], int(float(sys.argv[4]))
+    PREC = sys.argv[5] if len(sys.argv) > 5 else "f32"
+    key = config if PREC == "f32" else f"{config}_{PREC}"  # bench.py pmc_traffic key
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats_csv = os.path.join(src, "trace", "trace_kernel_stats.csv")
@@ -66,14 +74,14 @@ def main():
         wr = write.get(k, 0.0) * 1024
         per_launch[k] = {"read_bytes": rd, "write_bytes": wr, "total_bytes": rd + wr,
                          "raw_FETCH_SIZE_KB": fetch.get(k), "raw_WRITE_SIZE_KB": write.get(k)}
-    summary = {"tag": tag, "config": config, "symbols_per_launch": syms, "kernels": durations,
+    summary = {"tag": tag, "config": config, "precision": PREC, "symbols_per_launch": syms, "kernels": durations,
                "hbm_per_launch": per_launch,
                "correction": "read_bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write_bytes = WRITE_SIZE x 1024"}
     with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
     pm_path = os.path.join(prof, "pmc_summary.json")
     pm = json.load(open(pm_path)) if os.path.exists(pm_path) else {}
-    pm[config] = {"tag": tag, "symbols_per_launch": syms,
+    pm[key] = {"tag": tag, "symbols_per_launch": syms,
                   "bytes_per_launch": {k: v["total_bytes"] for k, v in per_launch.items()}}
     with open(pm_path, "w") as f:
         json.dump(pm, f, indent=1)
