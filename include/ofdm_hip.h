@@ -67,8 +67,8 @@ typedef struct ofdm_desc {
        subcarrier, which LUT it uses.  Fixed mode: one LUT, sc_lut == NULL.
        Adaptive mode (constellation/adaptive.py:16-91): n_luts LUTs and
        sc_lut[k] in [-1, n_luts) with -1 = inactive subcarrier (order 0). */
-    int32_t n_luts;              /* 0 = no constellation in this plan              */
-    const int32_t* lut_orders;   /* [n_luts] orders (perfect squares 4..256)       */
+    int32_t n_luts;              /* 0 = no constellation in this plan, at most 8   */
+    const int32_t* lut_orders;   /* [n_luts] orders (powers of two 2..256)         */
     const double* lut_pool;      /* concatenated LUTs, sum(lut_orders) complex      */
     const int32_t* sc_lut;       /* [n_fft] or NULL                                 */
     /* Channel: raw CIR (h_raw).  The plan normalises it to unit power for the

@@ -243,7 +243,7 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
     if (d->precision != OFDM_F32 && d->precision != OFDM_F64) return fail(OFDM_E_INVALID, "bad precision");
     if (d->equalizer < 0 || d->equalizer > 2) return fail(OFDM_E_INVALID, "bad equalizer");
     if (d->n_taps < 0 || d->n_taps > kMaxTaps) return fail(OFDM_E_INVALID, "n_taps must be in [0, 32]");
-    if (d->n_luts < 0 || d->n_luts > 4) return fail(OFDM_E_INVALID, "n_luts must be in [0, 4]");
+    if (d->n_luts < 0 || d->n_luts > kMaxLuts) return fail(OFDM_E_INVALID, "n_luts must be in [0, 8]");
 
     ofdm_plan_s* p = new ofdm_plan_s();
     std::unique_ptr<ofdm_plan_s> guard(p);
@@ -704,7 +704,6 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
 int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int64_t sym0, int64_t n_sym,
             void* y, ofdm_stats* stats) {
     if (!p || !p->has_const || p->L < 1) return fail(OFDM_E_INVALID, "ofdm_tx needs a constellation and channel taps");
-    if (!p->separable && p->adaptive) return fail(OFDM_E_INVALID, "adaptive loading needs square-QAM constellations");
     if (p->L - 1 > p->n) return fail(OFDM_E_INVALID, "fused path needs channel order <= n_fft");
     if (n_sym < 0 || sym0 < 0 || !stats) return fail(OFDM_E_INVALID, "bad argument to ofdm_tx");
     if (n_sym == 0) return OFDM_OK;
@@ -732,7 +731,6 @@ int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const 
             int64_t sym0, int64_t n_sym, int64_t n_valid_bits, uint64_t* counters, void* z_out,
             int64_t z_keep) {
     if (!p || !p->has_const) return fail(OFDM_E_INVALID, "ofdm_rx needs a constellation");
-    if (!p->separable && p->adaptive) return fail(OFDM_E_INVALID, "adaptive loading needs square-QAM constellations");
     if (p->eq != OFDM_EQ_NONE && !p->has_channel) return fail(OFDM_E_INVALID, "plan has no channel response");
     if (n_sym < 0 || sym0 < 0 || !counters) return fail(OFDM_E_INVALID, "bad argument to ofdm_rx");
     if (n_sym == 0) return OFDM_OK;  // an empty run (its stream has no samples and no noise power)

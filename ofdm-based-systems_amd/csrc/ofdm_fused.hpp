@@ -323,20 +323,21 @@ __device__ __forceinline__ uint32_t psk_decide(cpx<R> v, const TxRxCommon& cm) {
     return (uint32_t)(k ^ (k >> 1));
 }
 
-// Nearest constellation point of a non-separable LUT (PSK).  complex128: the reference's
-// |z - C_m| with hypot and the first index on ties (nn_index); complex64: the sector
-// decision above for the reference's M-PSK in throughput mode (cm.psk_m > 0 only there,
-// ofdm_abi.hip fill_common), else squared distances in float against the plan-precision LUT.
+// Nearest constellation point of a non-separable LUT (PSK): the m points at offset off of the
+// LUT pool (adaptive loading: the subcarrier's order; fixed: the whole single LUT).  complex128:
+// the reference's |z - C_m| with hypot and the first index on ties (nn_index); complex64: the
+// sector decision above for the reference's fixed M-PSK in throughput mode (cm.psk_m > 0 only
+// there, ofdm_abi.hip fill_common), else squared distances in float against the plan-precision LUT.
 template <typename R>
-__device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm) {
+__device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm, int off, int count) {
     if constexpr (sizeof(R) == 8) {
-        return (uint32_t)nn_index(v.re, v.im, cm.lut64, cm.lut_len);
+        return (uint32_t)nn_index(v.re, v.im, cm.lut64 + 2 * off, count);
     } else {
         if (cm.psk_m > 0) return psk_decide(v, cm);
-        const cpx<float>* L = (const cpx<float>*)cm.lut;
+        const cpx<float>* L = (const cpx<float>*)cm.lut + off;
         float bd = INFINITY;
         uint32_t best = 0;
-        for (int m = 0; m < cm.lut_len; ++m) {
+        for (int m = 0; m < count; ++m) {
             const float dr = v.re - L[m].re, di = v.im - L[m].im;
             const float d = dr * dr + di * di;
             if (d < bd) {
@@ -407,7 +408,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     C* lut = FB > 0 ? lut_s : cv.take<C>(cm.lut_len);
     C* h = cv.take<C>(32);
     C* hsw = cv.take<C>(WFIR ? 32 : 0);  // window FIR: the taps swizzled, (-im, re)
-    AxisInfo* axis = cv.take<AxisInfo>(4);
+    AxisInfo* axis = cv.take<AxisInfo>(kMaxLuts);
     unsigned char* rowmem = cv.take<unsigned char>((size_t)G::SPB * slot * (ROW_REAL ? sizeof(R) : sizeof(C)));
     C* tails = cv.take<C>((size_t)G::SPB * tls);
     uint32_t* words = cv.take<uint32_t>(FB ? 0 : (size_t)G::SPB * cm.words_per_sym);  // reference bits
@@ -771,7 +772,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     constexpr bool TT = uses_tt<R, LOGN, FB>();
     constexpr bool SPLIT = split_rows<R, FB>();  // complex128 throughput: rows of reals
     C* tw = cv.take<C>(TT ? 0 : 128);  // two-level twiddles (generic kernel, complex128 N > 1024)
-    AxisInfo* axis = cv.take<AxisInfo>(4);
+    AxisInfo* axis = cv.take<AxisInfo>(kMaxLuts);
     unsigned char* rowmem = cv.take<unsigned char>((size_t)G::SPB * G::PADN * (SPLIT ? sizeof(R) : sizeof(C)));
     uint32_t* words = cv.take<uint32_t>(FB ? 0 : (size_t)G::SPB * cm.words_per_sym);  // reference bits
     R* red = cv.take<R>(BLK / 64);
@@ -1080,11 +1081,13 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
                         if (sc.lut < 0) continue;
                         b = sc.bits;
                         off = sc.bitoff;
-                        ridx = slice<R>(v, axis[sc.lut]);
+                        // PSK orders (constellation/adaptive.py:130-265 with the PSK base mapper):
+                        // the nearest point of the subcarrier's own LUT
+                        ridx = nn ? nn_decide<R>(v, cm, axis[sc.lut].lut_off, 1 << sc.bits) : slice<R>(v, axis[sc.lut]);
                     } else {
                         b = cm.b;
                         off = k * b;
-                        ridx = nn ? nn_decide<R>(v, cm) : slicer(v);
+                        ridx = nn ? nn_decide<R>(v, cm, 0, cm.lut_len) : slicer(v);
                     }
                     uint32_t d = ridx ^ tb.generic(i, b, off);
                     ses += d != 0u;

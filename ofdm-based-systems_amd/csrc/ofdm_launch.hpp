@@ -24,6 +24,8 @@ constexpr int kMaxGrid = 4096;  // partial-sum workspace rows
 constexpr int kTxFields = 4;
 constexpr int kMaxTaps = 32;
 constexpr int kMaxLut = 512;
+// LUTs per plan: adaptive loading uses one per distinct order (PSK: 2 .. 256, eight orders)
+constexpr int kMaxLuts = 8;
 
 struct RowsArgs {
     const void* in;
@@ -190,7 +192,7 @@ inline size_t smem_tx(int logn, int blk, int lut_len, int wps, int L, int slot, 
     const int tls = L > 1 ? L - 1 : 1;
     if (fast) wps = 0;
     return rnd16((tts > 0 ? 0 : 128) * c) + rnd16((size_t)lut_len * c) + rnd16(32 * c) + rnd16(wfir ? 32 * c : 0) +
-           rnd16(4 * sizeof(AxisInfo)) +
+           rnd16(kMaxLuts * sizeof(AxisInfo)) +
            rnd16((size_t)spb * slot * (row_real ? sizeof(R) : c)) + rnd16((size_t)spb * tls * c) +
            rnd16((size_t)spb * wps * 4) + rnd16((size_t)(blk / 64) * sizeof(double)) + rnd16((size_t)tts * c) +
            rnd16(extra);
@@ -201,7 +203,7 @@ inline size_t smem_rx(int logn, int blk, int wps, int tts, size_t extra /* adapt
     const size_t c = 2 * sizeof(R);
     const int spb = geo_spb(logn, blk);
     if (fast) wps = 0;
-    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16(4 * sizeof(AxisInfo)) +
+    return rnd16((tts > 0 ? 0 : 128) * c) + rnd16(kMaxLuts * sizeof(AxisInfo)) +
            rnd16((size_t)spb * geo_padn(logn) * (row_real ? sizeof(R) : c)) + rnd16((size_t)spb * wps * 4) +
            rnd16((size_t)(blk / 64) * sizeof(R)) + rnd16((size_t)(blk / 64) * sizeof(unsigned long long)) +
            rnd16((size_t)tts * c) + rnd16(extra);

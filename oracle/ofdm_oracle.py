@@ -308,17 +308,32 @@ def qam_bit_loading_order(ser: float, snr: float) -> int:
     return 0 if b <= 0 else 2 ** b
 
 
+def psk_bit_loading_order(ser: float, snr: float) -> int:
+    """PSKConstellationMapper.calculate_bit_loading_order, constellation/models.py:460-474:
+    gamma* = Q^-1(SER/2)^2 / (2 pi^2), gamma = sqrt(snr gamma*) / (1 - sqrt(gamma* / (snr + 1e-10))),
+    b = floor(log2(1 + snr / (gamma + 1e-10)) + 1e-10), 0 if b <= 0."""
+    from scipy.stats import norm
+
+    q = norm.isf(ser / 2)
+    g_star = (q ** 2) / (2 * (np.pi ** 2))
+    gamma = (np.sqrt(snr * g_star)) / (1 - np.sqrt(g_star / (snr + 1e-10)))
+    b = int(np.floor(np.log2(1 + snr / (gamma + 1e-10)) + 1e-10))
+    return 0 if b <= 0 else 2 ** b
+
+
 # --------------------------------------------------------------------------- adaptive (CAPACITY_BASED)
 
 
-def adaptive_orders(N: int, h_raw: np.ndarray, snr_db: float, ser: float, waterfilling: bool):
-    """simulation/models.py:278-352: orders from the gap formula after power allocation (P_tot = N)."""
+def adaptive_orders(N: int, h_raw: np.ndarray, snr_db: float, ser: float, waterfilling: bool,
+                    scheme: str = "QAM"):
+    """simulation/models.py:278-352: orders from the base mapper's gap formula after power
+    allocation (P_tot = N); scheme "QAM" | "PSK" selects the base mapper class (:330-332)."""
     H = np.fft.fft(h_raw, N)
     g = np.abs(H) ** 2
     n0 = 10 ** (-snr_db / 10)
     p = waterfilling_allocation(N, g, n0) if waterfilling else uniform_allocation(N, N)
-    orders = np.array([qam_bit_loading_order(ser, pa * hg / n0) for pa, hg in zip(p, g)],
-                      dtype=np.int64)
+    rule = psk_bit_loading_order if scheme == "PSK" else qam_bit_loading_order
+    orders = np.array([rule(ser, pa * hg / n0) for pa, hg in zip(p, g)], dtype=np.int64)
     wl = None
     if waterfilling:
         wl = float(np.mean((p + n0 / g)[p > 1e-10]))
@@ -326,15 +341,17 @@ def adaptive_orders(N: int, h_raw: np.ndarray, snr_db: float, ser: float, waterf
 
 
 def run_adaptive(tx_bytes: bytes, orders: np.ndarray, N: int, h_raw: np.ndarray, cp: int, eq: str,
-                 snr_db: float, noise=None) -> LinkResult:
-    """CAPACITY_BASED data path: AdaptiveConstellationMapper.encode/decode (constellation/adaptive.py:130-265)."""
+                 snr_db: float, noise=None, scheme: str = "QAM") -> LinkResult:
+    """CAPACITY_BASED data path: AdaptiveConstellationMapper.encode/decode (constellation/adaptive.py:130-265)
+    over the base mapper's LUT per order (QAM or PSK)."""
     bps = np.array([int(np.log2(o)) if o > 0 else 0 for o in orders], dtype=np.int64)
     tot = int(bps.sum())
     tx_bits = bytes_to_bits(tx_bytes)
     if len(tx_bits) % tot:
         raise ValueError(f"Bits length ({len(tx_bits)}) must be multiple of bits_per_symbol ({tot})")
     S = len(tx_bits) // tot
-    luts = {int(o): qam_lut(int(o)) for o in np.unique(orders) if o > 0}
+    make = psk_lut if scheme == "PSK" else qam_lut
+    luts = {int(o): make(int(o)) for o in np.unique(orders) if o > 0}
     offs = np.concatenate([[0], np.cumsum(bps)[:-1]])
     bits2 = tx_bits.reshape(S, tot).astype(np.int64)
     idx = np.zeros((S, N), dtype=np.int64)

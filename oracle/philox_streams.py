@@ -212,7 +212,8 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
         orders = np.asarray(orders, np.int64)
         bk = np.array([int(np.log2(o)) if o > 0 else 0 for o in orders], np.int64)
         idx = tx_indices(gen, S, N, bk)
-        luts = {int(o): O.qam_lut(int(o)) for o in np.unique(orders) if o > 0}
+        make = O.psk_lut if scheme == "PSK" else O.qam_lut
+        luts = {int(o): make(int(o)) for o in np.unique(orders) if o > 0}
         X = np.zeros((S, N), np.complex128)
         for o, lt in luts.items():
             cols = orders == o
@@ -267,7 +268,7 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     if precision is not None:
         delta = z_error_bound(precision, Y, H, eq, snr_db, nerr, modulator, N)
         if orders is not None:
-            bracket = adaptive_bracket(Z, idx, orders, bk, delta)
+            bracket = adaptive_bracket(Z, idx, orders, bk, delta, scheme)
         else:
             bracket = decision_bracket(Z, idx, lut, b, delta, scheme)
     if orders is not None:
@@ -377,16 +378,13 @@ def _popcount(v: np.ndarray) -> np.ndarray:
     return np.bitwise_count(np.asarray(v, np.uint64)).astype(np.int64)
 
 
-def decision_bracket(Z: np.ndarray, idx: np.ndarray, lut: np.ndarray, b: int, delta: np.ndarray,
-                     scheme: str = "QAM") -> tuple:
-    """(bit_lo, bit_hi, sym_lo, sym_hi) over every decision of points within delta of Z.
-
-    QAM (the reference's square LUTs are separable): per axis the decided level
-    and, near an interior threshold, the level across it -- up to four candidate points.  PSK
-    (LUT[gray(i)] = exp(2 pi j i / M), constellation/models.py:356-380): the decided sector and,
-    when the point lies within delta of a sector boundary ray, the sector across it."""
+def decision_candidates(Z: np.ndarray, lut: np.ndarray, delta: np.ndarray, scheme: str = "QAM") -> list:
+    """Four candidate LUT indices per point (flattened): every decision of a point within delta
+    of Z.  QAM (the reference's square LUTs are separable): per axis the decided
+    level and, near an interior threshold, the level across it.  PSK (LUT[gray(i)] =
+    exp(2 pi j i / M), constellation/models.py:356-380): the decided sector and, when the point
+    lies within delta of a sector boundary ray, the sector across it (listed twice)."""
     Z = np.asarray(Z).ravel()
-    idx = np.asarray(idx).ravel().astype(np.int64)
     d = np.broadcast_to(delta, np.asarray(delta).shape).ravel()
     if scheme == "PSK":
         M = len(lut)
@@ -397,36 +395,42 @@ def decision_bracket(Z: np.ndarray, idx: np.ndarray, lut: np.ndarray, b: int, de
         dist = np.abs(Z) * np.sin(np.abs(np.abs(off) - w / 2))  # distance to the nearer boundary ray
         near = (dist <= d) & (M > 1)
         alt = np.mod(k + np.where(off >= 0, 1, -1), M)
-        gray = lambda v: v ^ (v >> 1)  # noqa: E731
-        cands = [gray(k), np.where(near, gray(alt), gray(k))]
-    else:
-        lev, step, table = _qam_levels(lut)
-        side = len(lev)
-        ki, ki2 = _axis_candidates(Z.real, lev[0], step, side, d)
-        kq, kq2 = _axis_candidates(Z.imag, lev[0], step, side, d)
-        cands = [table[kq, ki], table[kq, ki2], table[kq2, ki], table[kq2, ki2]]
+        g0, g1 = k ^ (k >> 1), np.where(near, alt ^ (alt >> 1), k ^ (k >> 1))
+        return [g0, g1, g0, g1]
+    lev, step, table = _qam_levels(lut)
+    side = len(lev)
+    ki, ki2 = _axis_candidates(Z.real, lev[0], step, side, d)
+    kq, kq2 = _axis_candidates(Z.imag, lev[0], step, side, d)
+    return [table[kq, ki], table[kq, ki2], table[kq2, ki], table[kq2, ki2]]
+
+
+def decision_bracket(Z: np.ndarray, idx: np.ndarray, lut: np.ndarray, b: int, delta: np.ndarray,
+                     scheme: str = "QAM") -> tuple:
+    """(bit_lo, bit_hi, sym_lo, sym_hi) over every decision of points within delta of Z
+    (decision_candidates)."""
+    idx = np.asarray(idx).ravel().astype(np.int64)
+    cands = decision_candidates(Z, lut, delta, scheme)
     be = np.stack([_popcount(c ^ idx) for c in cands])
     ne = np.stack([c != idx for c in cands])
     return (int(be.min(0).sum()), int(be.max(0).sum()), int(ne.all(0).sum()), int(ne.any(0).sum()))
 
 
 def adaptive_bracket(Z: np.ndarray, idx: np.ndarray, orders: np.ndarray, bk: np.ndarray,
-                     delta: np.ndarray) -> tuple:
-    """decision_bracket for CAPACITY_BASED loading: per order, the QAM candidates of its
-    subcarriers; bit errors counted as adaptive_counts does (trailing partial byte excluded)."""
+                     delta: np.ndarray, scheme: str = "QAM") -> tuple:
+    """decision_bracket for CAPACITY_BASED loading: per order, the candidates of its subcarriers
+    over that order's LUT (QAM or PSK); bit errors counted as adaptive_counts does (trailing
+    partial byte excluded)."""
     S, N = Z.shape
     d = np.broadcast_to(delta, (S, N))
     cand = [np.array(idx, np.int64) for _ in range(4)]
+    make = O.psk_lut if scheme == "PSK" else O.qam_lut
     for o in np.unique(orders):
         if o <= 0:
             continue
         cols = np.flatnonzero(orders == o)
-        lev, step, table = _qam_levels(O.qam_lut(int(o)))
-        zz, dd = Z[:, cols], d[:, cols]
-        ki, ki2 = _axis_candidates(zz.real, lev[0], step, len(lev), dd)
-        kq, kq2 = _axis_candidates(zz.imag, lev[0], step, len(lev), dd)
-        for c, (a_, b_) in zip(cand, ((kq, ki), (kq, ki2), (kq2, ki), (kq2, ki2))):
-            c[:, cols] = table[a_, b_]
+        cs = decision_candidates(Z[:, cols], make(int(o)), d[:, cols], scheme)
+        for c, v in zip(cand, cs):
+            c[:, cols] = v.reshape(S, len(cols))
     be0, _ = adaptive_counts((cand[0] ^ idx).astype(np.int64), bk, S)
     # the other candidates change an element's bit count by at most the spread of its popcounts
     diffs = np.stack([_popcount(c ^ idx) for c in cand])

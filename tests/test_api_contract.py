@@ -84,6 +84,8 @@ def test_bit_loading_orders_match_reference():
     for ser, vals in bl["orders"].items():
         got = [QAMConstellationMapper.calculate_bit_loading_order(ser=float(ser), snr=s) for s in bl["snrs"]]
         assert got == vals["qam"]
+        got = [PSKConstellationMapper.calculate_bit_loading_order(ser=float(ser), snr=s) for s in bl["snrs"]]
+        assert got == vals["psk"]
 
 
 # ----------------------------------------------------------------- serial / parallel (serial_parallel/models.py:6-21)

@@ -29,7 +29,7 @@ import philox_streams as P
 import ofdm_oracle as O
 from ofdm_based_systems import _backend as B
 from ofdm_based_systems.constellation.adaptive import AdaptiveConstellationMapper
-from ofdm_based_systems.constellation.models import QAMConstellationMapper
+from ofdm_based_systems.constellation.models import PSKConstellationMapper, QAMConstellationMapper
 from ofdm_based_systems.engine import LinkEngine, new_stats
 
 pytestmark = pytest.mark.gpu
@@ -96,6 +96,10 @@ CASES = [
     (256, 0, "two_ray", "MMSE", 1024, 16.0, B.OFDM_F32, {"adaptive": True}),  # unused subcarriers
     (4096, 0, "Lin-Phoong_P1", "MMSE", 160, 26.0, B.OFDM_F32, {"adaptive": True}),
     (64, 0, "default_multipath", "MMSE", 4097, 18.0, B.OFDM_F32, {"adaptive": True}),
+    # CAPACITY_BASED with the PSK base mapper (orders 2..32 and unused subcarriers at an aggressive
+    # SER target): the generic kernel, nearest point within each subcarrier's own LUT
+    (64, 0, "Lin-Phoong_P2", "MMSE", 1024, 20.0, B.OFDM_F32, {"adaptive": True, "scheme": "PSK", "ser": 0.1}),
+    (128, 0, "two_ray", "ZF", 511, 26.0, B.OFDM_F64, {"adaptive": True, "scheme": "PSK", "ser": 0.05}),
 ]
 
 
@@ -113,9 +117,12 @@ def setup(N, M, ch, eq, prec, var=None, snr=None):
     h = channel(ch)
     cp = var.pop("cp", len(h) - 1)
     sc = None
+    ser = var.pop("ser", 1e-3)
     if var.pop("adaptive", False):
-        orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
-        luts, sc = AdaptiveConstellationMapper(orders, QAMConstellationMapper, N).lut_tables()
+        psk = var.get("scheme") == "PSK"
+        orders, _, _ = O.adaptive_orders(N, h, snr, ser, True, "PSK" if psk else "QAM")
+        base = PSKConstellationMapper if psk else QAMConstellationMapper
+        luts, sc = AdaptiveConstellationMapper(orders, base, N).lut_tables()
         var["orders"] = orders
     else:
         luts = [O.psk_lut(M) if var.get("scheme") == "PSK" else O.qam_lut(M)]

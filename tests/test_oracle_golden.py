@@ -87,8 +87,9 @@ def test_adaptive_runs_match_reference(case):
     p, r = case["params"], case["result"]
     h = channel(case["channel"])
     N = p["num_subcarriers"]
+    scheme = p.get("constellation_scheme", "QAM")
     orders, power, wl = O.adaptive_orders(N, h, p["snr_db"], p.get("desired_symbol_error_rate", 1e-3),
-                                          p["power_allocation_type"] == "WATERFILLING")
+                                          p["power_allocation_type"] == "WATERFILLING", scheme)
     assert orders.tolist() == r["constellation_order_per_subcarrier"]
     np.testing.assert_array_equal(power, np.array(r["allocated_power"]))
     if wl is not None:
@@ -97,7 +98,7 @@ def test_adaptive_runs_match_reference(case):
     S = p["num_symbols"]
     cp = O.prefix_length(h, p["prefix_length_ratio"], "CP")
     tx, nz = O.reference_streams(case["seed"], bps * S, S * (N + cp))
-    res = O.run_adaptive(tx, orders, N, h, cp, p["equalizator_type"], p["snr_db"], nz)
+    res = O.run_adaptive(tx, orders, N, h, cp, p["equalizator_type"], p["snr_db"], nz, scheme)
     assert (res.bit_errors, res.symbol_errors, res.total_bits) == (
         r["bit_errors"], r["symbol_errors"], r["total_bits"])
     assert math.isclose(res.papr_db, r["papr_db"], rel_tol=1e-9)
@@ -123,3 +124,4 @@ def test_bit_loading_matches_reference():
     for ser, vals in bl["orders"].items():
         got = [O.qam_bit_loading_order(float(ser), s) for s in bl["snrs"]]
         assert got == vals["qam"]
+        assert [O.psk_bit_loading_order(float(ser), s) for s in bl["snrs"]] == vals["psk"]
