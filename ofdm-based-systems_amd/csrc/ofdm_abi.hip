@@ -281,7 +281,8 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
         if ((rc = upload_cpx(p->tw, tw, p->prec, s))) return rc;
     }
     // per-pass twiddle tables of the throughput kernels (ofdm_device.hpp tt_from):
-    // [forward | inverse], pass (LOGR, LOGNS > 0): T[(r-1) NS + k] = exp(-+2 pi i k r / (NS RAD))
+    // [forward | inverse], pass (LOGR, LOGNS > 0): T[(r-1) NS + k] = exp(-+2 pi i k r / (NS RAD)),
+    // r = 1 only for compact passes (tt_compact)
     if (p->logn > 4) {
         const int tts = tt_size(p->logn);
         std::vector<double> tt(4 * (size_t)tts, 0.0);
@@ -290,7 +291,8 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
             const int logr = std::min(4, p->logn - logns);
             const int ns = 1 << logns, rad = 1 << logr;
             if (logns > 0) {
-                for (int r = 1; r < rad; ++r)
+                const int rmax = tt_compact(p->logn, logns) ? 2 : rad;  // compact: W^k only
+                for (int r = 1; r < rmax; ++r)
                     for (int k = 0; k < ns; ++k, ++at) {
                         const double a = -2.0 * M_PI * (double)(k * r) / (double)(ns * rad);
                         tt[2 * at] = std::cos(a);

@@ -270,10 +270,20 @@ __device__ __forceinline__ int pad_plus(int padded_b) {
 // of butterfly k = j mod NS by W^(k r), W = exp(-+2 pi i / (NS RAD)); the tables hold
 // T[(r - 1) NS + k] for 0 < r < RAD, k < NS, pass after pass, computed on the host in
 // double.  One LDS read per twiddle instead of the two-level lookup and the recurrence.
+// Compact passes (NS >= 256 at N >= 2^OFDM_TT_COMPACT_MIN_LOGN: the last pass of N = 2048 / 4096)
+// hold only W^k for k < NS: the butterfly reads w = W^k and forms W^(k r) by recurrence (RAD - 2
+// complex products; <= 14 roundings, ~1e-6 in f32).  The full tables of those passes are 7/8 of
+// the total (28.7 of 32.6 KB at N = 4096 in complex64), which would otherwise cap a CU at two
+// workgroups.
+#ifndef OFDM_TT_COMPACT_MIN_LOGN
+#define OFDM_TT_COMPACT_MIN_LOGN 11
+#endif
+constexpr bool tt_compact(int logn, int logns) { return logn >= OFDM_TT_COMPACT_MIN_LOGN && logns >= 8; }
 constexpr int tt_from(int logn, int logns) {
     if (logns >= logn) return 0;
     const int logr = logn - logns >= 4 ? 4 : logn - logns;
-    return (logns > 0 ? ((1 << logr) - 1) << logns : 0) + tt_from(logn, logns + logr);
+    const int here = logns > 0 ? (tt_compact(logn, logns) ? 1 : (1 << logr) - 1) << logns : 0;
+    return here + tt_from(logn, logns + logr);
 }
 constexpr int tt_size(int logn) { return logn <= 4 ? 0 : tt_from(logn, 0); }
 
@@ -423,7 +433,15 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
     for (int q = 0; q < NB; ++q) {
         const int j = t + q * G::TPS;
         const int k = j & (NS - 1);
-        if constexpr (LOGNS > 0 && TT) {
+        if constexpr (LOGNS > 0 && TT && tt_compact(LOGN, LOGNS)) {
+            const cpx<R> w1 = tt[(tt_size(LOGN) - tt_from(LOGN, LOGNS)) + k];
+            cpx<R> wr = w1;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) {
+                v[q][r] = cmulv(wr, v[q][r]);
+                if (r + 1 < RAD) wr = cmulv(wr, w1);
+            }
+        } else if constexpr (LOGNS > 0 && TT) {
             const cpx<R>* T = tt + (tt_size(LOGN) - tt_from(LOGN, LOGNS)) + k;
 #pragma unroll
             for (int r = 1; r < RAD; ++r) v[q][r] = cmulv(T[(r - 1) * NS], v[q][r]);
@@ -478,7 +496,15 @@ __device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb,
     for (int q = 0; q < NB; ++q) {
         const int j = t + q * G::TPS;
         const int k = j & (NS - 1);
-        if constexpr (LOGNS > 0 && TT) {
+        if constexpr (LOGNS > 0 && TT && tt_compact(LOGN, LOGNS)) {
+            const cpx<R> w1 = tt[(tt_size(LOGN) - tt_from(LOGN, LOGNS)) + k];
+            cpx<R> wr = w1;
+#pragma unroll
+            for (int r = 1; r < RAD; ++r) {
+                v[q][r] = cmul(wr, v[q][r]);
+                if (r + 1 < RAD) wr = cmul(wr, w1);
+            }
+        } else if constexpr (LOGNS > 0 && TT) {
             const cpx<R>* T = tt + (tt_size(LOGN) - tt_from(LOGN, LOGNS)) + k;
 #pragma unroll
             for (int r = 1; r < RAD; ++r) v[q][r] = cmul(T[(r - 1) * NS], v[q][r]);
@@ -587,9 +613,10 @@ __device__ __forceinline__ void fft_reg_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb, 
 }
 
 // Twiddle source of the throughput kernels: per-pass LDS tables (complex64 always; complex128
-// while the table fits beside the rows, N <= 1024: 16 KB) or the two-level table plus recurrence.
+// while the table fits beside the rows, <= 16 KB: every N with the compact last passes) or the
+// two-level table plus recurrence.
 template <typename R, int LOGN>
-constexpr bool fast_tt() { return sizeof(R) == 4 || LOGN <= 10; }
+constexpr bool fast_tt() { return sizeof(R) == 4 || tt_size(LOGN) * 2 * (int)sizeof(R) <= 16384; }
 
 // b (<= 8) bits at bit offset o of a stream stored as 32-bit words, stream bit 32w+j
 // = bit (31-j) of word w; one word of slack after the stream.

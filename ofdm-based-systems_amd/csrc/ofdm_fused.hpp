@@ -151,6 +151,20 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 #ifndef OFDM_F64_FIR_BLOCK
 #define OFDM_F64_FIR_BLOCK 512
 #endif
+// complex64 throughput kernels at N >= 2048 (configs d, e): workgroup and waves per SIMD of RX
+// and of the window-FIR TX (two or four waves per symbol).  With the compact twiddle tables the
+// LDS no longer caps a CU at two workgroups, so 3 waves per SIMD fit: config e RX 3.37 -> 2.84 ms
+// per 2.5e5 symbols; N = 2048 (config d) prefers 768-thread workgroups (RX 3.08 -> 2.99 ms per
+// 5e5 symbols), N = 4096 256 (profiles/r03h_ab.txt)
+#ifndef OFDM_RX_BIG_BLOCK
+#define OFDM_RX_BIG_BLOCK(LOGN) ((LOGN) == 11 ? 768 : 256)
+#endif
+#ifndef OFDM_RX_BIG_WAVES
+#define OFDM_RX_BIG_WAVES 3
+#endif
+#ifndef OFDM_TX_BIG_WFIR_WAVES
+#define OFDM_TX_BIG_WFIR_WAVES 3
+#endif
 // LT (throughput TX): 0 flat channel; 4 / 8 multipath with <= LT taps through the register
 // window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps)
 template <typename R, int FB, int LOGN, int LT>
@@ -163,6 +177,7 @@ constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 template <typename R, int FB, int LOGN, int LT>
 constexpr int tx_waves() {
     if (sizeof(R) == 8 && FB > 0) return LT == 0 ? OFDM_F64_TX_WAVES : 2;
+    if (FB > 0 && LT > 0 && LOGN > 10) return OFDM_TX_BIG_WFIR_WAVES;
     return block_waves(tx_block<R, FB, LOGN, LT>(), FB > 0 && LT > 0 ? OFDM_TX_WFIR_WAVES : OFDM_TX_WAVES);
 }
 // padded FIR row index of the throughput multipath TX: one slot per 16 elements
@@ -184,13 +199,15 @@ template <typename R, int FB, int LOGN>
 constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB > 1 && LOGN >= 6 && LOGN <= 10; }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_block() {
-    if (sizeof(R) == 8 && FB > 0) return LOGN <= 10 ? OFDM_F64_RX_BLOCK : 512;
+    if (sizeof(R) == 8 && FB > 0) return LOGN > 10 ? 512 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_BLOCK : 768);
+    if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_BLOCK(LOGN);
     return rx_prefetch<R, FB, LOGN>() ? kBlock
                                        : (FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock);
 }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_waves() {
-    if (sizeof(R) == 8 && FB > 0) return LOGN <= 10 ? OFDM_F64_RX_WAVES : 2;
+    if (sizeof(R) == 8 && FB > 0) return LOGN > 10 ? 2 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_WAVES : 3);
+    if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;
     return rx_prefetch<R, FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
 }
 // throughput RX: equaliser coefficients staged in LDS up to N = 2^OFDM_EQ_LDS_MAX_LOGN (beyond,
