@@ -757,24 +757,37 @@ template <int FB>
 struct PermSlicer64 {
     static constexpr int SIDE = 1 << (FB / 2), HB = FB / 2;
     static constexpr uint32_t BYTE_MASK = 0x01010101u * ((1u << FB) - 1u);
-    double mul, add, smax;
+    double mul, add, smax, magic;
     uint32_t ti[4], tq[4];
 
+    // the constants are workgroup-uniform: held in SGPR pairs (readfirstlane), so each v_fma_f64
+    // takes one scalar operand instead of a VGPR copy
+    __device__ static double uniform(double x) {
+        const uint64_t u = __builtin_bit_cast(uint64_t, x);
+        // readfirstlane returns a signed int: widen through uint32_t, or bit 31 of the low word
+        // would sign-extend into the high word
+        const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u);
+        const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+        return __builtin_bit_cast(double, lo | (hi << 32));
+    }
     __device__ void load(const AxisInfo& a, double scale) {
         const double span = (double)(SIDE - 1);
-        mul = a.inv_step * scale / span;
-        add = -a.lev0 * a.inv_step / span;
+        mul = uniform(a.inv_step * scale / span);
+        add = a.lev0 * a.inv_step / span;  // negated in the FMA (neg modifier)
         smax = span;
+        magic = uniform(6755399441055744.0);  // 1.5 * 2^52
         for (int w = 0; w < 4; ++w) ti[w] = tq[w] = 0u;
         for (int k = 0; k < SIDE; ++k) {
             ti[k >> 2] |= (uint32_t)a.ipat[k] << (8 * (k & 3));
             tq[k >> 2] |= ((uint32_t)a.qpat[k] << HB) << (8 * (k & 3));
         }
     }
+    // Both FMAs in asm: written in C the second became an in-place v_fmac_f64 whose addend (the
+    // 1.5 * 2^52 constant) was rebuilt by two v_mov_b32 before every decision.
     __device__ __forceinline__ uint32_t level(double u) const {
-        double v;
-        asm("v_fma_f64 %0, %1, %2, %3 clamp" : "=v"(v) : "v"(u), "v"(mul), "v"(add));
-        const double f = __builtin_fma(v, smax, 6755399441055744.0);  // + 1.5 * 2^52
+        double v, f;
+        asm("v_fma_f64 %0, %1, %2, -%3 clamp" : "=v"(v) : "v"(u), "s"(mul), "v"(add));
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(f) : "v"(v), "v"(smax), "s"(magic));
         return (uint32_t)__builtin_bit_cast(uint64_t, f);
     }
     __device__ __forceinline__ uint32_t diff(const cpx<double> (&z)[4], uint32_t txw) const {

@@ -11,7 +11,10 @@ name) and saves the CSV text after every step, the file names of the constellati
 BER images it writes (``save_constellation_plot`` / ``plot_ber_vs_snr``) and the files
 mirrored under ``docs/figures``; plus ``main()``'s channel-directory naming for each
 settings file under ``config/`` and its return code for a missing configuration.
-Writes ``cli.json``.
+Also runs the reference's ``main()`` end to end on a reduced copy of
+``config/simulation_settings_test.json`` (``CLI_NUM_SYMBOLS`` constellation symbols, every SNR
+of the file), seeded as make_golden.seed_all does once before ``main()``, and keeps the
+``results/ber_results.csv`` it writes (``cli_run``).  Writes ``cli.json``.
 """
 
 from __future__ import annotations
@@ -44,6 +47,9 @@ IMAGES = [
     dict(prefix_type="NONE", modulation_type="OFDM", equalization_method="NONE", constellation_order=4,
          constellation_type="QAM", power_allocation="UNIFORM", snr_db=-3.0),
 ]
+
+CLI_NUM_SYMBOLS = 64 * 32
+CLI_SEED = 1
 
 BER_RESULTS = [
     {"prefix_acronym": "CP", "modulator_type": "OFDM", "equalizator_type": "MMSE", "constellation_order": 16,
@@ -82,6 +88,7 @@ def main() -> None:
             out["main_missing_config_stdout"] = buf.getvalue()
         finally:
             os.chdir(cwd)
+    out["cli_run"] = cli_run(ref_main)
     os.chdir(REF)
     try:
         for f in sorted(os.listdir("config")):
@@ -98,6 +105,37 @@ def main() -> None:
     with open(os.path.join(OUT, "cli.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     print("wrote cli.json")
+
+
+def cli_run(ref_main) -> dict:
+    """The reference's main() on the reduced test configuration, seeded once before the run:
+    the CSV of BER per SNR it writes."""
+    import shutil
+
+    import numpy as np
+    from numpy.random import PCG64, Generator
+
+    import ofdm_based_systems.bits_generation.models as bg
+
+    cfg = json.load(open(os.path.join(REF, "config", "simulation_settings_test.json")))
+    cfg["num_symbols"] = CLI_NUM_SYMBOLS
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.chdir(d)
+        try:
+            os.makedirs("config/channel_models")
+            shutil.copy(os.path.join(REF, "config", "settings.json"), "config/settings.json")
+            shutil.copy(os.path.join(REF, "config", "channel_models", "severe_multipath.npy"), "config/channel_models/")
+            json.dump(cfg, open("config/simulation_settings.json", "w"))
+            bg.RandomBitsGenerator.__init__.__defaults__ = (Generator(PCG64(CLI_SEED)),)
+            bg.AdaptiveBitsGenerator.__init__.__defaults__ = (Generator(PCG64(CLI_SEED)),)
+            np.random.seed(CLI_SEED)
+            with contextlib.redirect_stdout(io.StringIO()):
+                rc = ref_main.main()
+            csv = open("results/ber_results.csv").read()
+        finally:
+            os.chdir(cwd)
+    return {"num_symbols": CLI_NUM_SYMBOLS, "seed": CLI_SEED, "rc": rc, "csv": csv}
 
 
 if __name__ == "__main__":

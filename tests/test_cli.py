@@ -146,19 +146,32 @@ def test_runner_round_robin_two_ranks(tmp_path):
 
 @pytest.mark.gpu
 def test_cli_main_on_gpu(tmp_path, monkeypatch):
-    """``python -m ofdm_based_systems.main`` on a reduced copy of config/simulation_settings_test.json."""
+    """``python -m ofdm_based_systems.main`` on a reduced copy of config/simulation_settings_test.json,
+    seeded as the reference's main() was when tests/golden/make_cli_golden.py ran it: the same
+    results/ber_results.csv, byte for byte (BER per SNR from the GPU path), plus the image files."""
+    import numpy as np
+    from numpy.random import PCG64, Generator
+
+    import ofdm_based_systems.bits_generation.models as bg
+
+    want = G["cli_run"]
     monkeypatch.chdir(tmp_path)
     os.makedirs("config/channel_models")
     shutil.copy(os.path.join(ROOT, "config", "settings.json"), "config/settings.json")
     shutil.copy(os.path.join(ROOT, "config", "channel_models", "severe_multipath.npy"), "config/channel_models/")
     cfg = json.load(open(os.path.join(ROOT, "config", "simulation_settings_test.json")))
-    cfg["num_symbols"] = 64 * 32
+    cfg["num_symbols"] = want["num_symbols"]
     json.dump(cfg, open("config/simulation_settings.json", "w"))
-    assert M.main() == 0
-    lines = open("results/ber_results.csv").read().splitlines()
-    assert len(lines) == 1 + len(cfg["signal_noise_ratios"])
-    bers = [float(x.split(",")[2]) for x in lines[1:]]
-    assert all(0.0 <= b < 0.5 for b in bers)
+    defaults = (bg.RandomBitsGenerator.__init__.__defaults__, bg.AdaptiveBitsGenerator.__init__.__defaults__)
+    try:
+        bg.RandomBitsGenerator.__init__.__defaults__ = (Generator(PCG64(want["seed"])),)
+        bg.AdaptiveBitsGenerator.__init__.__defaults__ = (Generator(PCG64(want["seed"])),)
+        np.random.seed(want["seed"])
+        assert M.main() == want["rc"] == 0
+    finally:
+        bg.RandomBitsGenerator.__init__.__defaults__, bg.AdaptiveBitsGenerator.__init__.__defaults__ = defaults
+    assert open("results/ber_results.csv").read() == want["csv"]
+    assert float(want["csv"].splitlines()[1].split(",")[2]) > 0  # a run with errors to compare
     imgs = os.listdir("images/severe_multipath")
     assert len(imgs) == 1 + len(cfg["signal_noise_ratios"]) and any(i.endswith("BER_vs_SNR.png") for i in imgs)
     assert sorted(os.listdir("docs/figures/severe_multipath")) == sorted(imgs)
