@@ -200,17 +200,17 @@ int psk_order(const double* lut, int m) {
     return m;
 }
 
-// Diagnostic ablation switches for timing studies (tools/ablate.py), read only by OFDM_ABLATION
-// builds; the product library runs every launch in full whatever the environment holds.
-int env_flags(const char* name) {
 #if OFDM_ABLATION
+// Diagnostic ablation switches for timing studies (tools/ablate.py), compiled only into
+// OFDM_ABLATION builds: the product library has no environment-controlled work skipping.
+int env_flags(const char* name) {
     const char* v = std::getenv(name);
     return v ? std::atoi(v) : 0;
-#else
-    (void)name;
-    return 0;
-#endif
 }
+#define OFDM_ENV_FLAGS(name) env_flags(name)
+#else
+#define OFDM_ENV_FLAGS(name) 0
+#endif
 
 int log2_exact(int n) {
     int l = 0;
@@ -719,7 +719,7 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
     a.L = p->L;
     a.chunk = p->L > 1 ? 16 : 1;
     a.slot = tx_slot(p->logn, p->cp, p->L);
-    a.flags = env_flags("OFDM_ABLATE_TX");
+    a.flags = OFDM_ENV_FLAGS("OFDM_ABLATE_TX");
     int grid = 0;  // chosen by the launcher with the kernel (<= kMaxGrid partial records)
 #define CALL(R) launch_tx<R>(p->logn, a, &grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));
@@ -751,7 +751,7 @@ int ofdm_rx(ofdm_plan_t p, void* stream, const void* y, const double* nr, const 
     a.counters = counters;
     a.z_out = z_out;
     a.z_keep = z_out ? z_keep : 0;
-    a.flags = env_flags("OFDM_ABLATE_RX");
+    a.flags = OFDM_ENV_FLAGS("OFDM_ABLATE_RX");
     int grid = 0;
 #define CALL(R) launch_rx<R>(p->logn, a, &grid, (hipStream_t)stream)
     HIPCHK(DISPATCH(p, CALL));

@@ -82,3 +82,11 @@ def test_product_has_no_cpu_fallback():
 
     with pytest.raises(B.BackendUnavailable):
         QAMConstellationMapper(16).decode(np.zeros(4, np.complex128))
+
+
+def test_product_library_has_no_ablation_switches():
+    """The timing tools' OFDM_ABLATE_TX / _RX switches (work skipping inside the kernels) are
+    compiled only into -DOFDM_ABLATION=1 builds: the product library never reads them."""
+    with open(B.lib_path(), "rb") as f:
+        blob = f.read()
+    assert b"OFDM_ABLATE" not in blob
