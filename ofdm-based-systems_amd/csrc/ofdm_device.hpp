@@ -835,6 +835,29 @@ struct OrderParams {
 };
 constexpr int kUnusedOrder = 7;
 
+// (rx ^ tx) of four elements from their levels (li: I axis, lq: Q axis on -Im z, level in the low
+// byte), per-order meta words and the lane word: U lookups, Q bits moved up by b_j / 2, tx mask
+template <bool SMALL>
+__device__ __forceinline__ uint32_t adaptive_combine(const uint32_t (&li)[4], const uint32_t (&lq)[4],
+                                                     const uint32_t (&meta)[4], uint32_t txw) {
+    const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
+                                              __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
+    const uint32_t sq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(lq[3], lq[2], 0x0c0c0400u),
+                                              __builtin_amdgcn_perm(lq[1], lq[0], 0x0c0c0400u), 0x05040100u);
+    const uint32_t ib = upat_lookup<SMALL>(si), qb = upat_lookup<SMALL>(sq);
+    // Q bits << b_j/2 per byte: bytes 0, 2 and 1, 3 as u16 pairs through v_pk_mul_lo_u16
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t w02 = __builtin_amdgcn_perm(0u, qb, 0x0c020c00u), w13 = __builtin_amdgcn_perm(0u, qb, 0x0c030c01u);
+    const uint32_t f02 = __builtin_amdgcn_perm(meta[2], meta[0], 0x0c050c01u);
+    const uint32_t f13 = __builtin_amdgcn_perm(meta[3], meta[1], 0x0c050c01u);
+    const uint32_t p02 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, w02) * __builtin_bit_cast(u16x2, f02));
+    const uint32_t p13 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, w13) * __builtin_bit_cast(u16x2, f13));
+    const uint32_t qs = __builtin_amdgcn_perm(p13, p02, 0x06020400u);
+    const uint32_t mw = __builtin_amdgcn_perm(__builtin_amdgcn_perm(meta[3], meta[2], 0x0c0c0400u),
+                                              __builtin_amdgcn_perm(meta[1], meta[0], 0x0c0c0400u), 0x05040100u);
+    return (ib | qs) ^ (txw & mw);
+}
+
 // (rx ^ tx) of four elements of possibly different orders, one per byte.  op[j] = the
 // element's order entry, txw = the lane word; mask_out = the tx masks (byte j).  SMALL: every
 // order of the plan is <= 64 (levels < 8: one v_perm per U lookup).
@@ -880,22 +903,7 @@ __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], cons
         asm("" : "+v"(li[j]), "+v"(lq[j]));
         meta[j] = op[j]->meta;
     }
-    const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
-                                              __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
-    const uint32_t sq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(lq[3], lq[2], 0x0c0c0400u),
-                                              __builtin_amdgcn_perm(lq[1], lq[0], 0x0c0c0400u), 0x05040100u);
-    const uint32_t ib = upat_lookup<SMALL>(si), qb = upat_lookup<SMALL>(sq);
-    // Q bits << b_j/2 per byte: bytes 0, 2 and 1, 3 as u16 pairs through v_pk_mul_lo_u16
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-    const uint32_t w02 = __builtin_amdgcn_perm(0u, qb, 0x0c020c00u), w13 = __builtin_amdgcn_perm(0u, qb, 0x0c030c01u);
-    const uint32_t f02 = __builtin_amdgcn_perm(meta[2], meta[0], 0x0c050c01u);
-    const uint32_t f13 = __builtin_amdgcn_perm(meta[3], meta[1], 0x0c050c01u);
-    const uint32_t p02 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, w02) * __builtin_bit_cast(u16x2, f02));
-    const uint32_t p13 = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, w13) * __builtin_bit_cast(u16x2, f13));
-    const uint32_t qs = __builtin_amdgcn_perm(p13, p02, 0x06020400u);
-    const uint32_t mw = __builtin_amdgcn_perm(__builtin_amdgcn_perm(meta[3], meta[2], 0x0c0c0400u),
-                                              __builtin_amdgcn_perm(meta[1], meta[0], 0x0c0c0400u), 0x05040100u);
-    return (ib | qs) ^ (txw & mw);
+    return adaptive_combine<SMALL>(li, lq, meta, txw);
 }
 
 // ------------------------------------------------------------------ exact power sums
@@ -919,6 +927,34 @@ __host__ __device__ inline void fx_normalize(unsigned long long& l0, unsigned lo
 }
 __host__ __device__ inline double fx_value(unsigned long long l0, unsigned long long l1) {
     return (double)l1 * kFxHi + (double)l0 * kFxLo;
+}
+
+// complex128 adaptive slicer: per-order constants in double (entries of 32 bytes, so the byte
+// offsets of the eight entries still fit the per-element code bytes), the same decisions and
+// bit handling as adaptive_diff; both FMAs of each axis in asm (the clamp bit, and no in-place
+// v_fmac rebuilding the rounding constant).
+struct OrderParams64 {
+    double mul, add, smax;  // level coordinate / (side - 1) = z mul - add, clamped; times smax
+    uint32_t meta, pad;
+};
+template <bool SMALL>
+__device__ __forceinline__ uint32_t adaptive_diff64(const cpx<double> (&z)[4], const OrderParams64* const (&op)[4],
+                                                    uint32_t txw, double magic) {
+    uint32_t li[4], lq[4], meta[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const OrderParams64& o = *op[j];
+        double vi, vq, fi, fq;
+        asm("v_fma_f64 %0, %1, %2, -%3 clamp" : "=v"(vi) : "v"(z[j].re), "v"(o.mul), "v"(o.add));
+        asm("v_fma_f64 %0, -%1, %2, -%3 clamp" : "=v"(vq) : "v"(z[j].im), "v"(o.mul), "v"(o.add));
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fi) : "v"(vi), "v"(o.smax), "s"(magic));
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fq) : "v"(vq), "v"(o.smax), "s"(magic));
+        li[j] = (uint32_t)__builtin_bit_cast(uint64_t, fi);
+        lq[j] = (uint32_t)__builtin_bit_cast(uint64_t, fq);
+        asm("" : "+v"(li[j]), "+v"(lq[j]));
+        meta[j] = o.meta;
+    }
+    return adaptive_combine<SMALL>(li, lq, meta, txw);
 }
 
 // ------------------------------------------------------------------ reductions

@@ -199,14 +199,15 @@ template <typename R, int FB, int LOGN>
 constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB > 1 && LOGN >= 6 && LOGN <= 10; }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_block() {
-    if (sizeof(R) == 8 && FB > 0) return LOGN > 10 ? 512 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_BLOCK : 768);
+    // (the adaptive kernel's per-order tables take ~200 VGPRs in complex128: 2 waves per SIMD)
+    if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 512 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_BLOCK : 768);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_BLOCK(LOGN);
     return rx_prefetch<R, FB, LOGN>() ? kBlock
                                        : (FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock);
 }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_waves() {
-    if (sizeof(R) == 8 && FB > 0) return LOGN > 10 ? 2 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_WAVES : 3);
+    if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 2 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_WAVES : 3);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;
     return rx_prefetch<R, FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
 }
@@ -218,8 +219,12 @@ constexpr int rx_waves() {
 #ifndef OFDM_EQ_PRE
 #define OFDM_EQ_PRE 1
 #endif
-template <int FB, int LOGN, int EQ>
-constexpr bool eq_in_lds() { return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= OFDM_EQ_LDS_MAX_LOGN; }
+// complex128 at N = 4096: the table (64 KB) fits beside two symbols' split rows and the compact
+// twiddles, and preloading 16 complex128 coefficients would spill
+template <typename R, int FB, int LOGN, int EQ>
+constexpr bool eq_in_lds() {
+    return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= (sizeof(R) == 8 ? 12 : OFDM_EQ_LDS_MAX_LOGN);
+}
 // complex128 throughput kernels exchange FFT data through rows of reals (fft_reg_split)
 template <typename R, int FB>
 constexpr bool split_rows() { return sizeof(R) == 8 && FB > 0; }
@@ -798,11 +803,13 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     // throughput kernel: forward per-pass twiddles, plus the inverse ones for SC-OFDM's IFFT
     const int tts_all = FB > 1 && scm ? 2 * TTS : TTS;
     C* tt = cv.take<C>(tts_all);
-    OrderParams* ordt = cv.take<OrderParams>(FB == 1 ? 8 : 0);  // adaptive: per-order slicer
+    // adaptive: per-order slicer constants (complex128: double entries)
+    using OP = std::conditional_t<sizeof(R) == 8, OrderParams64, OrderParams>;
+    OP* ordt = cv.take<OP>(FB == 1 ? 8 : 0);
     // throughput kernels with an equaliser: the per-subcarrier coefficient staged in LDS once
     // per workgroup (ZF: 1/H; MMSE: conj(H), |H|^2 recomputed from it) -- read from the plan's
     // global table, every element paid an L2 round trip with a vmcnt(0) per symbol
-    constexpr bool EQ_LDS = eq_in_lds<FB, LOGN, EQ>();
+    constexpr bool EQ_LDS = eq_in_lds<R, FB, LOGN, EQ>();
     C* eqt = cv.take<C>(EQ_LDS ? N : 0);
     // otherwise (throughput kernels at N = 4096, and the complex64 generic kernel) the lane's
     // coefficients are loaded before the FFT each symbol (L2-resident), so their latency hides
@@ -824,7 +831,20 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     if constexpr (EQ_LDS)
         for (int k = threadIdx.x; k < N; k += BLK) eqt[k] = ((const C*)cm.eq_a)[k];
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
-    if constexpr (FB == 1) {
+    if constexpr (FB == 1 && sizeof(R) == 8) {
+        if (threadIdx.x < 8) {
+            OrderParams64 o{0.0, 0.0, 0.0, 0u, 0u};  // unused subcarrier: level 0, no bits
+            if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
+                const AxisInfo ax = cm.axis[threadIdx.x];
+                const double span = (double)(ax.side - 1);
+                o.mul = ax.inv_step * cm.scale / span;  // the FFT output stays unscaled
+                o.add = ax.lev0 * ax.inv_step / span;   // negated in the FMA
+                o.smax = span;
+                o.meta = ((1u << ax.bits) - 1u) | ((1u << ax.hbits) << 8);
+            }
+            ordt[threadIdx.x] = o;
+        }
+    } else if constexpr (FB == 1) {
         if (threadIdx.x < 8) {
             // unused subcarrier: level 0, no bits
             OrderParams o{0.f, 0.f, OFDM_SLICER_CLAMP ? 0u : 0x4B400000u, 0u};
@@ -872,6 +892,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     // elements per word (the lane's subcarriers do not change from symbol to symbol)
     uint32_t ocode[FB == 1 ? E / 4 : 1];
     bool small_orders = false;  // adaptive: every order <= 64 (3-bit levels)
+    const double magic64 = PermSlicer64<2>::uniform(6755399441055744.0);  // 1.5 * 2^52 (complex128)
     if constexpr (FB == 1) {
         int side = 0;
         for (int l = 0; l < cm.n_axis; ++l) side = max(side, (int)axis[l].side);
@@ -882,7 +903,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int lid = cm.sc[t + (4 * q + j) * TPS].lut;
-                w |= (uint32_t)(sizeof(OrderParams) * (lid < 0 ? kUnusedOrder : lid)) << (8 * j);
+                w |= (uint32_t)(sizeof(OP) * (lid < 0 ? kUnusedOrder : lid)) << (8 * j);
             }
             ocode[q] = w;
         }
@@ -1036,16 +1057,21 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
                 static_for<0, E / 4>([&](auto Q) {
                     constexpr int q = Q;
                     C z[4];
-                    const OrderParams* op[4];
+                    const OP* op[4];
                     uint32_t oc = ocode[q];
                     asm volatile("" : "+v"(oc));
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         z[j] = equalized(4 * q + j);
-                        op[j] = (const OrderParams*)((const unsigned char*)ordt + ((oc >> (8 * j)) & 0xFFu));
+                        op[j] = (const OP*)((const unsigned char*)ordt + ((oc >> (8 * j)) & 0xFFu));
                     }
-                    uint32_t d = small_orders ? adaptive_diff<true>(z, op, lane_word(tb.lane, q))
-                                              : adaptive_diff<false>(z, op, lane_word(tb.lane, q));
+                    uint32_t d;
+                    if constexpr (sizeof(R) == 8)
+                        d = small_orders ? adaptive_diff64<true>(z, op, lane_word(tb.lane, q), magic64)
+                                         : adaptive_diff64<false>(z, op, lane_word(tb.lane, q), magic64);
+                    else
+                        d = small_orders ? adaptive_diff<true>(z, op, lane_word(tb.lane, q))
+                                         : adaptive_diff<false>(z, op, lane_word(tb.lane, q));
                     ses += PermSlicer<8>::nonzero_bytes(d);
                     if (!all_valid) {
                         // a trailing partial byte of the run is not compared (constellation/

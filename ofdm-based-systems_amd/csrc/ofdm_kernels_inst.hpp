@@ -189,7 +189,10 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
-        // complex128 throughput kernels: square QAM, device bits, OFDM with a cyclic prefix
+        // complex128 throughput kernels: square QAM (fixed or adaptive loading), device bits, OFDM
+        // with a cyclic prefix
+        if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
+            return tx_fast<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && !a.c.nn && !a.c.scm && !a.c.zpad) {
 #define OFDM_TX_FB64(F) \
     case F:                \
@@ -237,8 +240,8 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     constexpr int BLK = rx_block<R, FB, LOGN, EQ>();
     const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym,
                                  uses_tt<R, LOGN, FB>() ? tt_size(LOGN) * (FB > 1 && a.c.scm ? 2 : 1) : 0,
-                                 (FB == 1 ? 8 * sizeof(OrderParams) : 0) +
-                                     (eq_in_lds<FB, LOGN, EQ>() ? ((size_t)2 * sizeof(R)) << LOGN : 0),
+                                 (FB == 1 ? 8 * (sizeof(R) == 8 ? sizeof(OrderParams64) : sizeof(OrderParams)) : 0) +
+                                     (eq_in_lds<R, FB, LOGN, EQ>() ? ((size_t)2 * sizeof(R)) << LOGN : 0),
                                  FB > 0, split_rows<R, FB>());
     auto fn = k_rx<R, LOGN, EQ, FB>;
     hipError_t e = set_smem(fn, sm);
@@ -262,6 +265,9 @@ static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN>
 static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
+        if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
+            !a.c.scm && !a.c.zpad && !a.c.nn)
+            return rx_eq<R, LOGN, 1>(a, grid, s);
         if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr && !a.c.nn && !a.c.scm &&
             !a.c.zpad) {
 #define OFDM_RX_FB64(F) \
