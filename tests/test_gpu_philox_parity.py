@@ -99,7 +99,7 @@ CASES = [
     # ... and on the complex128 adaptive throughput kernel (FB = 1, double per-order tables)
     (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F64, {"adaptive": True}),
     (256, 0, "two_ray", "ZF", 1023, 30.0, B.OFDM_F64, {"adaptive": True}),
-    (1024, 0, "severe_multipath", "NONE", 257, 26.0, B.OFDM_F64, {"adaptive": True}),
+    (1024, 0, "severe_multipath", "ZF", 257, 24.0, B.OFDM_F64, {"adaptive": True}),
     # CAPACITY_BASED with the PSK base mapper (orders 2..32 and unused subcarriers at an aggressive
     # SER target): the generic kernel, nearest point within each subcarrier's own LUT
     (64, 0, "Lin-Phoong_P2", "MMSE", 1024, 20.0, B.OFDM_F32, {"adaptive": True, "scheme": "PSK", "ser": 0.1}),
