@@ -135,7 +135,7 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 // registers: 16 complex128 elements per lane plus a radix-16 butterfly -- RX ~160 VGPRs (3 waves
 // per SIMD: one 768-thread workgroup of 12 symbols per CU), flat TX 128 (4 waves: 1024 threads).
 // The FIR TX keeps complex rows (the FIR window reads the extended stream): 512 threads at
-// 2 waves per SIMD, 256 below N = 1024 where 512 threads' rows exceed the LDS.
+// 2 waves per SIMD, 256 where 512 threads' rows exceed the LDS.
 #ifndef OFDM_F64_TX_BLOCK
 #define OFDM_F64_TX_BLOCK 1024
 #endif
@@ -170,7 +170,9 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 template <typename R, int FB, int LOGN, int LT>
 constexpr int tx_block() {
     if (sizeof(R) == 8 && FB > 0)
-        return LT == 0 ? OFDM_F64_TX_BLOCK : (LOGN < 10 ? 256 : OFDM_F64_FIR_BLOCK);
+        // (FIR rows of complex128 plus, adaptive, the 8 KB LUT pool and the per-subcarrier table:
+        // 512 threads exceed the LDS below N = 1024 and for adaptive loading from N = 2048)
+        return LT == 0 ? OFDM_F64_TX_BLOCK : ((LOGN < 10 || (FB == 1 && LOGN >= 11)) ? 256 : OFDM_F64_FIR_BLOCK);
     return FB > 0 && LOGN <= 10 ? (LT != 0 ? OFDM_TX_MP_BLOCK : OFDM_TX_FAST_BLOCK) : kBlock;
 }
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
