@@ -165,14 +165,22 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 #ifndef OFDM_TX_BIG_WFIR_WAVES
 #define OFDM_TX_BIG_WFIR_WAVES 3
 #endif
+// LDS of the complex128 FIR TX at blk threads (upper estimate of its Carve sequence, smem_tx):
+// complex FIR rows of fir_pad(N + 32) + 1 slots and the 7-sample tails per symbol, per-pass
+// twiddles, the static LUT (adaptive: the 512-entry pool and the per-subcarrier table), taps
+constexpr int f64_fir_lds(int fb, int logn, int blk) {
+    const int n = 1 << logn, tps = logn < 4 ? 1 : n >> 4, spb = blk / tps;
+    const int rows = spb * ((n + 32) + ((n + 32) >> 4) + 1 + 7) * 16;
+    const int tt = tt_size(logn) * 16;
+    const int lut = fb == 1 ? (kMaxLut + 1) * 16 + 4 * n : (16 << fb);
+    return rows + tt + lut + 1024;
+}
 // LT (throughput TX): 0 flat channel; 4 / 8 multipath with <= LT taps through the register
 // window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps)
 template <typename R, int FB, int LOGN, int LT>
 constexpr int tx_block() {
     if (sizeof(R) == 8 && FB > 0)
-        // (FIR rows of complex128 plus, adaptive, the 8 KB LUT pool and the per-subcarrier table:
-        // 512 threads exceed the LDS below N = 1024 and for adaptive loading from N = 2048)
-        return LT == 0 ? OFDM_F64_TX_BLOCK : ((LOGN < 10 || (FB == 1 && LOGN >= 11)) ? 256 : OFDM_F64_FIR_BLOCK);
+        return LT == 0 ? OFDM_F64_TX_BLOCK : (f64_fir_lds(FB, LOGN, OFDM_F64_FIR_BLOCK) <= 160 * 1024 ? OFDM_F64_FIR_BLOCK : 256);
     return FB > 0 && LOGN <= 10 ? (LT != 0 ? OFDM_TX_MP_BLOCK : OFDM_TX_FAST_BLOCK) : kBlock;
 }
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
