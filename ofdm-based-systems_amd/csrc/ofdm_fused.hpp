@@ -134,6 +134,8 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 // imaginary rows (fft_reg_split: 8.5 KB per N = 1024 symbol), so the occupancy is set by the
 // registers: 16 complex128 elements per lane plus a radix-16 butterfly -- RX ~160 VGPRs (3 waves
 // per SIMD: one 768-thread workgroup of 12 symbols per CU), flat TX 128 (4 waves: 1024 threads).
+// A 4-wave RX (1024 threads, 128 VGPRs, 7 spilled) measured config b 1.646 -> 1.648e8 symbols/s,
+// within the run-to-run spread (profiles/r03k_ab_rx1024.txt): not taken.
 // The FIR TX keeps complex rows (the FIR window reads the extended stream): 512 threads at
 // 2 waves per SIMD, 256 where 512 threads' rows exceed the LDS.
 #ifndef OFDM_F64_TX_BLOCK
