@@ -4,6 +4,9 @@
 #pragma once
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "ofdm_kernels.hpp"
 
@@ -44,24 +47,27 @@ static inline int clamp_grid(int64_t want) {
 #define OFDM_PERSISTENT 0
 #endif
 // Persistent grid for a grid-stride kernel: as many workgroups as the device holds at once
-// (occupancy x CUs, queried once per kernel and device), so no partial last round of
-// workgroups idles part of the chip.
+// (occupancy x CUs), so no partial last round of workgroups idles part of the chip.  Cached per
+// kernel (its address: every instantiation has the same function type), device, workgroup size
+// and dynamic LDS.
 template <typename F>
 static int resident_grid(F fn, int blk, size_t smem) {
-    static int cached[16] = {0};
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, int, size_t>, int> cached;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-    if (cached[dev] == 0) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), blk, smem) !=
-                hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-            (void)hipGetLastError();
-            return kMaxGrid;
-        }
-        cached[dev] = std::max(1, std::min(kMaxGrid, per_cu * cus));
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    const auto key = std::make_tuple(reinterpret_cast<const void*>(fn), dev, blk, smem);
+    std::lock_guard<std::mutex> lock(mu);
+    const auto it = cached.find(key);
+    if (it != cached.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), blk, smem) !=
+            hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return kMaxGrid;
     }
-    return cached[dev];
+    return cached[key] = std::max(1, std::min(kMaxGrid, per_cu * cus));
 }
 
 template <typename R, int LOGN, int MODE>

@@ -164,16 +164,22 @@ def _pipelined_worker(rank, world, port, out):
     for sd in seeds:
         eng.seed_streams(sd, c["S"])
     piped = [p.result() for p in eng.run_pipelined(c["S"], c["snr"], seeds, group=dist.group.WORLD)]
+    # a y budget below two shards' buffers: the runs go through batched run_async instead
+    # (16 KB: 8 of a rank's 24 symbols per batch)
+    small = [p.result() for p in eng.run_pipelined(c["S"], c["snr"], seeds, group=dist.group.WORLD,
+                                                   y_budget=8 * c["N"] * 16)]
     serial = [eng.run(c["S"], c["snr"], seed=sd, group=dist.group.WORLD) for sd in seeds]
     out[rank] = ([(r.bit_errors, r.symbol_errors, r.power_sum) for r in piped],
-                 [(r.bit_errors, r.symbol_errors, r.power_sum) for r in serial])
+                 [(r.bit_errors, r.symbol_errors, r.power_sum) for r in serial],
+                 [(r.bit_errors, r.symbol_errors, r.power_sum) for r in small])
     dist.destroy_process_group()
 
 
 def test_pipelined_runs_match_serial_runs():
     """bench.py's schedule (run k+1's TX enqueued before run k's RX, asynchronous exchanges)
     gives every run the counts and statistics of LinkEngine.run with the same seed, on every
-    rank, and those of the single-process oracle."""
+    rank, and those of the single-process oracle; so does its batched fallback when the two
+    runs' channel-sample buffers exceed y_budget."""
     c = CASE
     h = channel(c["ch"])
     cp = len(h) - 1
@@ -181,8 +187,9 @@ def test_pipelined_runs_match_serial_runs():
     out = mp.Manager().dict()
     mp.spawn(_pipelined_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     for r in range(2):
-        piped, serial = out[r]
+        piped, serial, small = out[r]
         assert piped == serial, (r, piped, serial)
+        assert small == serial, (r, small, serial)
     for k, sd in enumerate([11, 12, 13]):
         tx, nz = O.reference_streams(sd, c["S"] * c["N"] * b, c["S"] * (c["N"] + cp))
         ref = O.run_fixed(tx, c["S"] * c["N"] * b, c["N"], c["M"], h, cp, c["eq"], c["snr"], nz)
