@@ -97,6 +97,7 @@ struct ofdm_plan_s {
     int adaptive, b, bps, n_axis, lut_len, n_active;
     double gain_mean;
     DevBuf tw, ptw, lut, lut64, h, eq_a, eq_b, axis, sc, active, H64;
+    double gtap[3][kWinTaps];  // normalised taps in Gauss form (TxArgs::gtap)
     // partial-sum workspaces (3 x kMaxGrid doubles), one per HIP stream the plan has been
     // used on: launches on different streams may run concurrently, and a reduction's
     // partials must not be overwritten by another stream's kernel before k_finalize reads
@@ -370,6 +371,12 @@ int ofdm_plan_create(ofdm_plan_t* out, const ofdm_desc* d, void* stream) {
         std::vector<double> hn(2 * d->n_taps);
         for (int l = 0; l < 2 * d->n_taps; ++l) hn[l] = d->h_raw[l] / sc;
         if ((rc = upload_cpx(p->h, hn, p->prec, s))) return rc;
+        for (int l = 0; l < kWinTaps; ++l) {
+            const double re = l < d->n_taps ? hn[2 * l] : 0.0, im = l < d->n_taps ? hn[2 * l + 1] : 0.0;
+            p->gtap[0][l] = re;
+            p->gtap[1][l] = re + im;
+            p->gtap[2][l] = im - re;
+        }
     }
     if (p->has_channel) {
         if (hipMalloc(&p->H64.p, 16 * (size_t)p->n) != hipSuccess) return fail(OFDM_E_ALLOC, "hipMalloc failed");
@@ -717,6 +724,7 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
     if (!a.partials) return fail(OFDM_E_ALLOC, "hipMalloc failed");
     a.h = p->h.p;
     a.L = p->L;
+    std::memcpy(a.gtap, p->gtap, sizeof a.gtap);
     a.chunk = p->L > 1 ? 16 : 1;
     a.slot = tx_slot(p->logn, p->cp, p->L);
     a.flags = OFDM_ENV_FLAGS("OFDM_ABLATE_TX");

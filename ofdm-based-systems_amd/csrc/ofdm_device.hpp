@@ -1144,7 +1144,9 @@ struct Mwc64x {
     // complex128 kernels: the same radius and phase entry, the product taken in double against
     // ntab64 = the float32 table entries widened (exact), fused into the sample: one conversion
     // and two v_fma_f64 instead of a float product and two conversions.  Bits 3..8 of w address
-    // the 16-byte entries as (w & 0x1F8) * 2.
+    // the 16-byte entries as (w & 0x1F8) * 2.  (16 copies of the table, one per 16-byte bank slot
+    // so that a ds_read_b128 lane group never meets on a bank, measured slower: config b RX
+    // 3.07 -> 3.25 ms, profiles/r03m_ab.txt.)
     __device__ __forceinline__ void add_noise64(double& re, double& im, const f64x2* ntab64) {
         const uint32_t w = next();
         const float r = noise_radius(w);

@@ -474,7 +474,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     if (threadIdx.x < 32) {
         const C hq = threadIdx.x < L ? ((const C*)a.h)[threadIdx.x] : mk<R>(0, 0);
         h[threadIdx.x] = hq;
-        if (WFIR) hsw[threadIdx.x] = mk<R>(-hq.im, hq.re);
+        if (WFIR) hsw[threadIdx.x] = mk<R>(-hq.im, hq.re);  // window FIR (complex64): taps swizzled
     }
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     __syncthreads();
@@ -626,32 +626,60 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                 sym_sync<TPS>();
                 if constexpr (sizeof(R) == 8) {
                     if (active && c >= 0) {
-                        // complex128: the same register window, one complex FMA chain per output
-                        // (4 v_fma_f64 per tap)
-                        int ho = 0;
-                        asm volatile("" : "+v"(ho));
-                        C hq[LT];
+                        // complex128: the same register window, each output in Gauss's
+                        // three-multiplication form with the products accumulated as sums:
+                        //   T = sum hr (wr + wi),  U = sum (hr + hi) wi,  V = sum (hi - hr) wr,
+                        //   y = (T - U, T + V)
+                        // -- 3 v_fma_f64 per tap plus 2 adds per output and 1 per window sample,
+                        // instead of the 4 of a complex FMA.  The taps' three forms come with the
+                        // kernel arguments (TxArgs::gtap, zero past L) and stay in scalar registers:
+                        // the window and the accumulators fill the vector registers at LT = 8
+                        static_assert(LT <= kWinTaps, "window FIR taps");
+                        R hr[LT], c1[LT], c2[LT];
 #pragma unroll
-                        for (int q = 0; q < LT; ++q) hq[q] = h[ho + q];
+                        for (int q = 0; q < LT; ++q) {
+                            hr[q] = a.gtap[0][q];
+                            c1[q] = a.gtap[1][q];
+                            c2[q] = a.gtap[2][q];
+                        }
                         const C* wb = row + (A + (A >> 4) + 17 * t);
-                        C win[WN];
+                        R wre[WN], wim[WN], wsum[WN];
 #pragma unroll
-                        for (int w = 0; w < WN; ++w) win[w] = wb[w + (w >> 4)];
+                        for (int w = 0; w < WN; ++w) {
+                            const C ev = wb[w + (w >> 4)];
+                            wre[w] = ev.re;
+                            wim[w] = ev.im;
+                            wsum[w] = ev.re + ev.im;
+                        }
                         R pys = 0;
                         C* yo = yout + sl * N + E * t;
 #pragma unroll
                         for (int j = 0; j < E; ++j) {
-                            C yv = mk<R>(0, 0);
+                            R T = 0, U = 0, V = 0;
 #pragma unroll
-                            for (int l = 0; l < LT; ++l) yv = yv + cmul(hq[l], win[j + LT - 1 - l]);
-                            pys += norm2(yv);
+                            for (int l = 0; l < LT; ++l) {
+                                const int w = j + LT - 1 - l;
+                                T = __builtin_fma(hr[l], wsum[w], T);
+                                U = __builtin_fma(c1[l], wim[w], U);
+                                V = __builtin_fma(c2[l], wre[w], V);
+                            }
+                            const C yv = mk<R>(T - U, T + V);
+                            pys = __builtin_fma(yv.re, yv.re, pys);
+                            pys = __builtin_fma(yv.im, yv.im, pys);
                             if (yout && !(flags & 4)) yo[j] = yv;
                         }
                         if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
-                            C yp = mk<R>(0, 0);
+                            R T = 0, U = 0, V = 0;
 #pragma unroll
-                            for (int l = 0; l < LT; ++l) yp = yp + cmul(hq[l], row[fir_pad(R0 + t - l)]);
-                            pys += norm2(yp);
+                            for (int l = 0; l < LT; ++l) {
+                                const C ev = row[fir_pad(R0 + t - l)];
+                                T = __builtin_fma(hr[l], ev.re + ev.im, T);
+                                U = __builtin_fma(c1[l], ev.im, U);
+                                V = __builtin_fma(c2[l], ev.re, V);
+                            }
+                            const R pr = T - U, pi = T + V;
+                            pys = __builtin_fma(pr, pr, pys);
+                            pys = __builtin_fma(pi, pi, pys);
                         }
                         fx_accum((double)pys, pq0, pq1);
                     }
@@ -931,12 +959,20 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     const int64_t niter = (cm.n_sym + G::SPB - 1) / G::SPB;
     unsigned long long be = 0, se = 0;
 
-    // kept channel samples of local symbol sl (zeros past the end / when ablated)
+    // kept channel samples of local symbol sl.  Past the end the wave reads the last symbol
+    // again (its results are neither counted nor stored): an unconditional load, where zeroing
+    // the 16 elements cost 32 v_mov_b64 per symbol in complex128.  Zeros when ablated.
     auto load_sym = [&](int64_t sl, C (&dst)[E]) {
-        const C* ys = (const C*)a.y + sl * ystride;
-        if (sl < cm.n_sym && !(flags & 16)) {
+        const C* ys = (const C*)a.y + (sl < cm.n_sym ? sl : cm.n_sym - 1) * ystride;
+        if (!(flags & 16)) {
+            // issued in element order, the order the noise consumes them: each add then waits
+            // for its own load only (left to the scheduler, the N = 4096 complex128 RX issued
+            // element 0 thirteenth and waited for 13 of 16 loads before its first add)
 #pragma unroll
-            for (int i = 0; i < E; ++i) dst[i] = ld_stream<(FB > 0 && OFDM_RX_NT)>(ys + t + i * TPS);
+            for (int i = 0; i < E; ++i) {
+                dst[i] = ld_stream<(FB > 0 && OFDM_RX_NT)>(ys + t + i * TPS);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         } else {
 #pragma unroll
             for (int i = 0; i < E; ++i) dst[i] = mk<R>(0, 0);

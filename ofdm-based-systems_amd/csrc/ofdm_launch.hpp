@@ -23,6 +23,7 @@ constexpr int kMaxGrid = 4096;  // partial-sum workspace rows
 // fused TX partials per workgroup: sum |y|^2 as fixed-point limbs (2 x u64), sum |x|^2, max |x|^2
 constexpr int kTxFields = 4;
 constexpr int kMaxTaps = 32;
+constexpr int kWinTaps = 8;  // taps of the register-window FIR (LT = 4 / 8)
 constexpr int kMaxLut = 512;
 // LUTs per plan: adaptive loading uses one per distinct order (PSK: 2 .. 256, eight orders)
 constexpr int kMaxLuts = 8;
@@ -143,6 +144,9 @@ struct TxArgs {
     int slot;   // complex elements per symbol row in LDS
     int flags;  // diagnostic ablation (OFDM_ABLATION builds, OFDM_ABLATE_TX): 1 no bit staging, 2 no FFT,
                 // 4 no y store
+    // complex128 window FIR: the first kWinTaps taps in Gauss form (re, re + im, im - re), read
+    // from the kernel arguments into scalar registers (the taps are wave-uniform)
+    double gtap[3][kWinTaps];
 };
 
 struct RxArgs {
