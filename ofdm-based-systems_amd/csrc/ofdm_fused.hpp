@@ -136,8 +136,12 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 // per SIMD: one 768-thread workgroup of 12 symbols per CU), flat TX 128 (4 waves: 1024 threads).
 // A 4-wave RX (1024 threads, 128 VGPRs, 7 spilled) measured config b 1.646 -> 1.648e8 symbols/s,
 // within the run-to-run spread (profiles/r03k_ab_rx1024.txt): not taken.
-// The FIR TX keeps complex rows (the FIR window reads the extended stream): 512 threads at
-// 2 waves per SIMD, 256 where 512 threads' rows exceed the LDS.
+// The window-FIR TX passes the extended stream through its row of reals twice (real, then
+// imaginary parts), in 256-thread workgroups at 2 waves per SIMD: two or more workgroups per
+// CU, so a symbol group's barriers (N >= 2048: TPS > 64) hold back fewer waves.  Against
+// complex rows at 512 threads (256 where they did not fit, 1 wave per SIMD): TX per step
+// c 5.45 -> 5.37, d 7.01 -> 5.41, e 6.37 -> 5.39 ms; rows of reals at 512 threads measured
+// 5.59 / 6.67 / 6.65 (profiles/r03o_ab.txt).
 #ifndef OFDM_F64_TX_BLOCK
 #define OFDM_F64_TX_BLOCK 1024
 #endif
@@ -151,7 +155,7 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 #define OFDM_F64_RX_WAVES 3
 #endif
 #ifndef OFDM_F64_FIR_BLOCK
-#define OFDM_F64_FIR_BLOCK 512
+#define OFDM_F64_FIR_BLOCK 256
 #endif
 // complex64 throughput kernels at N >= 2048 (configs d, e): workgroup and waves per SIMD of RX
 // and of the window-FIR TX (two or four waves per symbol).  With the compact twiddle tables the
@@ -168,11 +172,12 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 #define OFDM_TX_BIG_WFIR_WAVES 3
 #endif
 // LDS of the complex128 FIR TX at blk threads (upper estimate of its Carve sequence, smem_tx):
-// complex FIR rows of fir_pad(N + 32) + 1 slots and the 7-sample tails per symbol, per-pass
+// FIR rows of fir_pad(N + 32) + 1 reals (window FIR; the run-time-tap FIR: complex) and the 7
+// complex tail samples per symbol, per-pass
 // twiddles, the static LUT (adaptive: the 512-entry pool and the per-subcarrier table), taps
-constexpr int f64_fir_lds(int fb, int logn, int blk) {
+constexpr int f64_fir_lds(int fb, int logn, int blk, bool real_rows) {
     const int n = 1 << logn, tps = logn < 4 ? 1 : n >> 4, spb = blk / tps;
-    const int rows = spb * ((n + 32) + ((n + 32) >> 4) + 1 + 7) * 16;
+    const int rows = spb * (((n + 32) + ((n + 32) >> 4) + 1) * (real_rows ? 8 : 16) + 7 * 16);
     const int tt = tt_size(logn) * 16;
     const int lut = fb == 1 ? (kMaxLut + 1) * 16 + 4 * n : (16 << fb);
     return rows + tt + lut + 1024;
@@ -182,7 +187,8 @@ constexpr int f64_fir_lds(int fb, int logn, int blk) {
 template <typename R, int FB, int LOGN, int LT>
 constexpr int tx_block() {
     if (sizeof(R) == 8 && FB > 0)
-        return LT == 0 ? OFDM_F64_TX_BLOCK : (f64_fir_lds(FB, LOGN, OFDM_F64_FIR_BLOCK) <= 160 * 1024 ? OFDM_F64_FIR_BLOCK : 256);
+        return LT == 0 ? OFDM_F64_TX_BLOCK
+                       : (f64_fir_lds(FB, LOGN, OFDM_F64_FIR_BLOCK, LT > 0) <= 160 * 1024 ? OFDM_F64_FIR_BLOCK : 256);
     return FB > 0 && LOGN <= 10 ? (LT != 0 ? OFDM_TX_MP_BLOCK : OFDM_TX_FAST_BLOCK) : kBlock;
 }
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
@@ -430,8 +436,9 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     const int slot = a.slot;  // complex elements per symbol row (>= PADN and >= L-1+cp+N)
     const int tls = L > 1 ? L - 1 : 1;
     constexpr bool TT = uses_tt<R, LOGN, FB>();
-    // complex128 flat TX: the row only carries the FFT exchange, a row of reals (fft_reg_split)
-    constexpr bool ROW_REAL = split_rows<R, FB>() && LT == 0;
+    // complex128 flat and window-FIR TX: a row of reals (fft_reg_split)
+    // (the window FIR passes its stream through the row of reals twice: real, then imaginary parts)
+    constexpr bool ROW_REAL = split_rows<R, FB>() && LT >= 0;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(TT ? 0 : 128);  // two-level twiddles (generic kernel, complex128 N > 1024)
     // throughput kernels: the LUT in static LDS at a link-time address, so an element's LUT read
@@ -611,46 +618,71 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                 // free; offsets compile-time) -- 23 LDS reads instead of 2 L per output
                 static_assert(E == 16 && TPS >= 16, "window FIR geometry");
                 constexpr int WN = E + LT - 1;
-                sym_sync<TPS>();  // the last FFT pass has read the row
-                {
-                    const int u = R0 + cp + t;  // stream sample cp + t + TPS i at fir_pad(u + TPS i)
-                    const int bx = fir_pad(u);
-#pragma unroll
-                    for (int i = 0; i < E; ++i) row[bx + TPS * i + (TPS * i >> 4)] = x[i];  // TPS i = 0 mod 16
-                }
-                if (t >= TPS - cp) row[fir_pad(R0 + t - (TPS - cp))] = x[E - 1];  // cyclic prefix
-                if (t < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
-                    const int z = t - (LT - L);
-                    row[fir_pad(R0 - (LT - 1) + t)] = z < 0 ? mk<R>(0, 0) : tl[z];
-                }
-                sym_sync<TPS>();
                 if constexpr (sizeof(R) == 8) {
-                    if (active && c >= 0) {
-                        // complex128: the same register window, each output in Gauss's
-                        // three-multiplication form with the products accumulated as sums:
-                        //   T = sum hr (wr + wi),  U = sum (hr + hi) wi,  V = sum (hi - hr) wr,
-                        //   y = (T - U, T + V)
-                        // -- 3 v_fma_f64 per tap plus 2 adds per output and 1 per window sample,
-                        // instead of the 4 of a complex FMA.  The taps' three forms come with the
-                        // kernel arguments (TxArgs::gtap, zero past L) and stay in scalar registers:
-                        // the window and the accumulators fill the vector registers at LT = 8
-                        static_assert(LT <= kWinTaps, "window FIR taps");
-                        R hr[LT], c1[LT], c2[LT];
+                    // complex128: the row is a row of reals (half the LDS of a complex row: two
+                    // symbols per CU more at N >= 2048), so the stream goes through it twice, real
+                    // parts then imaginary parts, into the same register window.  Each output in
+                    // Gauss's three-multiplication form with the products accumulated as sums:
+                    //   T = sum hr (wr + wi),  U = sum (hr + hi) wi,  V = sum (hi - hr) wr,
+                    //   y = (T - U, T + V)
+                    // -- 3 v_fma_f64 per tap plus 2 adds per output and 1 per window sample,
+                    // instead of the 4 of a complex FMA.  The taps' three forms come with the
+                    // kernel arguments (TxArgs::gtap, zero past L) and stay in scalar registers:
+                    // the window and the accumulators fill the vector registers at LT = 8
+                    static_assert(LT <= kWinTaps, "window FIR taps");
+                    R* rr = (R*)row;
+                    const bool live = active && c >= 0;
+                    R hr[LT], c1[LT], c2[LT];
 #pragma unroll
-                        for (int q = 0; q < LT; ++q) {
-                            hr[q] = a.gtap[0][q];
-                            c1[q] = a.gtap[1][q];
-                            c2[q] = a.gtap[2][q];
-                        }
-                        const C* wb = row + (A + (A >> 4) + 17 * t);
-                        R wre[WN], wim[WN], wsum[WN];
+                    for (int q = 0; q < LT; ++q) {
+                        hr[q] = a.gtap[0][q];
+                        c1[q] = a.gtap[1][q];
+                        c2[q] = a.gtap[2][q];
+                    }
+                    R wre[WN], wim[WN];
+                    R pT = 0, pU = 0, pV = 0;  // prefix-region output of lane t < cp
 #pragma unroll
-                        for (int w = 0; w < WN; ++w) {
-                            const C ev = wb[w + (w >> 4)];
-                            wre[w] = ev.re;
-                            wim[w] = ev.im;
-                            wsum[w] = ev.re + ev.im;
+                    for (int P = 0; P < 2; ++P) {  // P = 0: real parts, 1: imaginary parts
+                        const bool IM = P == 1;
+                        sym_sync<TPS>();  // the FFT's last pass / the real parts' reads are done
+                        {
+                            const int bx = fir_pad(R0 + cp + t);  // stream sample cp + t + TPS i
+#pragma unroll
+                            for (int i = 0; i < E; ++i) rr[bx + TPS * i + (TPS * i >> 4)] = IM ? x[i].im : x[i].re;
                         }
+                        if (t >= TPS - cp) rr[fir_pad(R0 + t - (TPS - cp))] = IM ? x[E - 1].im : x[E - 1].re;  // cyclic prefix
+                        if (t < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
+                            const int z = t - (LT - L);
+                            rr[fir_pad(R0 - (LT - 1) + t)] = z < 0 ? (R)0 : (IM ? tl[z].im : tl[z].re);
+                        }
+                        sym_sync<TPS>();
+                        {
+                            // every lane reads its window, live or not: read under the same
+                            // condition as the outputs, the two windows spilled (87-131 VGPRs)
+                            const R* wb = rr + (A + (A >> 4) + 17 * t);
+#pragma unroll
+                            for (int w = 0; w < WN; ++w) {
+                                if (IM) wim[w] = wb[w + (w >> 4)];
+                                else wre[w] = wb[w + (w >> 4)];
+                            }
+                            if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
+#pragma unroll
+                                for (int l = 0; l < LT; ++l) {
+                                    const R e = rr[fir_pad(R0 + t - l)];
+                                    pT = __builtin_fma(hr[l], e, pT);
+                                    if (IM) pU = __builtin_fma(c1[l], e, pU);
+                                    else pV = __builtin_fma(c2[l], e, pV);
+                                }
+                            }
+                        }
+                        // this symbol's tail for the next one (every lane has copied the old one)
+                        if (t < L - 1) {
+                            const R v = active ? rr[fir_pad(R0 + N + cp - (L - 1) + t)] : (R)0;
+                            if (IM) tl[t].im = v;
+                            else tl[t].re = v;
+                        }
+                    }
+                    if (live) {
                         R pys = 0;
                         C* yo = yout + sl * N + E * t;
 #pragma unroll
@@ -659,7 +691,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
 #pragma unroll
                             for (int l = 0; l < LT; ++l) {
                                 const int w = j + LT - 1 - l;
-                                T = __builtin_fma(hr[l], wsum[w], T);
+                                T = __builtin_fma(hr[l], wre[w] + wim[w], T);
                                 U = __builtin_fma(c1[l], wim[w], U);
                                 V = __builtin_fma(c2[l], wre[w], V);
                             }
@@ -668,22 +700,28 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             pys = __builtin_fma(yv.im, yv.im, pys);
                             if (yout && !(flags & 4)) yo[j] = yv;
                         }
-                        if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
-                            R T = 0, U = 0, V = 0;
-#pragma unroll
-                            for (int l = 0; l < LT; ++l) {
-                                const C ev = row[fir_pad(R0 + t - l)];
-                                T = __builtin_fma(hr[l], ev.re + ev.im, T);
-                                U = __builtin_fma(c1[l], ev.im, U);
-                                V = __builtin_fma(c2[l], ev.re, V);
-                            }
-                            const R pr = T - U, pi = T + V;
+                        if (t < cp) {
+                            const R pr = pT - pU, pi = pT + pV;
                             pys = __builtin_fma(pr, pr, pys);
                             pys = __builtin_fma(pi, pi, pys);
                         }
                         fx_accum((double)pys, pq0, pq1);
                     }
+                    sym_sync<TPS>();
                 } else {
+                    sym_sync<TPS>();  // the last FFT pass has read the row
+                    {
+                        const int u = R0 + cp + t;  // stream sample cp + t + TPS i at fir_pad(u + TPS i)
+                        const int bx = fir_pad(u);
+#pragma unroll
+                        for (int i = 0; i < E; ++i) row[bx + TPS * i + (TPS * i >> 4)] = x[i];  // TPS i = 0 mod 16
+                    }
+                    if (t >= TPS - cp) row[fir_pad(R0 + t - (TPS - cp))] = x[E - 1];  // cyclic prefix
+                    if (t < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
+                        const int z = t - (LT - L);
+                        row[fir_pad(R0 - (LT - 1) + t)] = z < 0 ? mk<R>(0, 0) : tl[z];
+                    }
+                    sym_sync<TPS>();
                     if (sizeof(R) == 4 && active && c >= 0) {
                         // taps (zero past L), LDS broadcast reads; the opaque offset keeps the reads
                         // in the symbol loop (hoisted, the 4 LT registers stay live through the FFT
@@ -734,10 +772,10 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         }
                         fx_accum((double)pys, pq0, pq1);
                     }
+                    // tail for the next symbol: the last L-1 stream samples (zeros before symbol 0)
+                    if (t < L - 1) tl[t] = active ? row[fir_pad(R0 + N + cp - (L - 1) + t)] : mk<R>(0, 0);
+                    sym_sync<TPS>();
                 }
-                // tail for the next symbol: the last L-1 stream samples (zeros before symbol 0)
-                if (t < L - 1) tl[t] = active ? row[fir_pad(R0 + N + cp - (L - 1) + t)] : mk<R>(0, 0);
-                sym_sync<TPS>();
             } else {
                 // extended serial stream in the row: [tail (L-1) | prefix (cp) | x (N)], or with
                 // zero padding [tail (L-1) | x (N) | zeros (cp)]

@@ -163,7 +163,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     }
     const size_t sm = smem_tx<R>(LOGN, BLK, FB > 0 ? 0 : a.c.lut_len, a.c.words_per_sym, a.L, a.slot,
                                  uses_tt<R, LOGN, FB>() ? tt_size(LOGN) : 0, FB > 0 && LT > 0,
-                                 FB == 1 ? (size_t)4 << LOGN : 0, FB > 0, split_rows<R, FB>() && LT == 0);
+                                 FB == 1 ? (size_t)4 << LOGN : 0, FB > 0, split_rows<R, FB>() && LT >= 0);
     auto fn = k_tx<R, LOGN, FB, LT>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
