@@ -54,13 +54,17 @@
 
 // Streaming (nontemporal) loads of the channel samples in RX: y is read exactly once, and
 // the nontemporal hint lifts the achievable read rate of this access pattern on MI355X from
-// 6.2 to 7.1 TB/s (tools/hbm_probe.hip).  TX stores: the same hint, off by default (no gain
-// measured on the write side).
+// 6.2 to 7.1 TB/s (tools/hbm_probe.hip).  TX stores: the same hint, off for complex64 (no gain
+// measured on the write side), on for the complex128 flat TX (config b TX 3.10 -> 3.00 ms,
+// profiles/r03r_ab.txt; not on the window-FIR TX's lane-contiguous stores).
 #ifndef OFDM_RX_NT
 #define OFDM_RX_NT 1
 #endif
 #ifndef OFDM_TX_NT
 #define OFDM_TX_NT 0
+#endif
+#ifndef OFDM_TX_NT_F64
+#define OFDM_TX_NT_F64 1
 #endif
 
 namespace ofdm {
@@ -172,12 +176,14 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 #define OFDM_TX_BIG_WFIR_WAVES 3
 #endif
 // LDS of the complex128 FIR TX at blk threads (upper estimate of its Carve sequence, smem_tx):
-// FIR rows of fir_pad(N + 32) + 1 reals (window FIR; the run-time-tap FIR: complex) and the 7
+// FIR rows of fir_pad(N + 32) + 1 reals (window FIR: or the N / 2 transposed outputs, if more;
+// the run-time-tap FIR: complex) and the 7
 // complex tail samples per symbol, per-pass
 // twiddles, the static LUT (adaptive: the 512-entry pool and the per-subcarrier table), taps
 constexpr int f64_fir_lds(int fb, int logn, int blk, bool real_rows) {
     const int n = 1 << logn, tps = logn < 4 ? 1 : n >> 4, spb = blk / tps;
-    const int rows = spb * (((n + 32) + ((n + 32) >> 4) + 1) * (real_rows ? 8 : 16) + 7 * 16);
+    const int fir = (n + 32) + ((n + 32) >> 4) + 1, transpose = 2 * (n / 2 + n / 16);
+    const int rows = spb * ((real_rows ? (fir > transpose ? fir : transpose) * 8 : fir * 16) + 7 * 16);
     const int tt = tt_size(logn) * 16;
     const int lut = fb == 1 ? (kMaxLut + 1) * 16 + 4 * n : (16 << fb);
     return rows + tt + lut + 1024;
@@ -200,6 +206,9 @@ constexpr int tx_waves() {
 }
 // padded FIR row index of the throughput multipath TX: one slot per 16 elements
 __host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
+// complex128 window-FIR TX: slot of output kk (of N / 2) in the row while it is transposed
+// for the store: one pad slot per 8, so the lanes' stride-8 writes fall on distinct banks
+__host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
 // Throughput RX (FB > 1, N <= 1024) software-pipelines its HBM loads: while a wave works on
 // one symbol, the channel samples of its next symbol are already in flight into registers
 // (E more VGPR pairs), so the load latency overlaps the FFT / noise / slicer instead of
@@ -414,6 +423,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     TxArgs a) {
     constexpr int BLK = tx_block<R, FB, LOGN, LT>();
     constexpr bool WFIR = FB > 0 && LT > 0;  // register window FIR
+    constexpr bool TX_NT = OFDM_TX_NT || (sizeof(R) == 8 && OFDM_TX_NT_F64);  // nontemporal y stores
     using G = Geo<LOGN, BLK>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
@@ -591,9 +601,9 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             // SGPR-base + 32-bit lane-offset form instead of a loop-carried 64-bit
                             // VGPR pointer (which spilled to scratch, and whose per-symbol reload's
                             // vmcnt(0) waited for all of the previous symbol's stores)
-                            st_stream<OFDM_TX_NT>(lane_ptr(uniform_ptr(yo), (uint32_t)(t + i * TPS)), yv);
+                            st_stream<TX_NT>(lane_ptr(uniform_ptr(yo), (uint32_t)(t + i * TPS)), yv);
                         } else {
-                            st_stream<(FB > 0 && OFDM_TX_NT)>(yo + t + i * TPS, yv);
+                            st_stream<(FB > 0 && TX_NT)>(yo + t + i * TPS, yv);
                         }
                     }
                     if (zp && yout)
@@ -682,11 +692,24 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             else tl[t].re = v;
                         }
                     }
-                    if (live) {
-                        R pys = 0;
-                        C* yo = yout + sl * N + E * t;
+                    // The lane's outputs are the 16 consecutive samples k = 16 t + j: stored
+                    // directly, every store instruction would touch 64 cache lines (the
+                    // stores cost config e 1.7 ms of 5.7, profiles/r03t_ablate_e.txt).  They
+                    // go through the row instead, in two halves (j < 8, j >= 8), each N / 2
+                    // complex samples at wfir_slot(kk), kk = 8 t + j % 8, and leave as
+                    // kk = t + TPS i: lanes 8 m .. 8 m + 7 store one whole 128-byte line.
+                    C* crow = (C*)rr;
+                    C* ys = yout + sl * N;
+                    const bool store = live && yout && !(flags & 4);
+                    R pys = 0;
 #pragma unroll
-                        for (int j = 0; j < E; ++j) {
+                    for (int hh = 0; hh < 2; ++hh) {
+                        sym_sync<TPS>();  // the windows / the previous half's samples are read
+                        // (every lane computes, live or not, as it read its window: under the
+                        // live condition the windows spilled)
+#pragma unroll
+                        for (int jj = 0; jj < 8; ++jj) {
+                            const int j = 8 * hh + jj;
                             R T = 0, U = 0, V = 0;
 #pragma unroll
                             for (int l = 0; l < LT; ++l) {
@@ -698,8 +721,23 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             const C yv = mk<R>(T - U, T + V);
                             pys = __builtin_fma(yv.re, yv.re, pys);
                             pys = __builtin_fma(yv.im, yv.im, pys);
-                            if (yout && !(flags & 4)) yo[j] = yv;
+                            crow[wfir_slot(8 * t + jj)] = yv;
                         }
+                        sym_sync<TPS>();
+                        if (store) {
+                            // lane offsets from an opaque copy of t: hoisted out of the symbol
+                            // loop they would hold 16 registers through the FFT
+                            int to = t;
+                            asm volatile("" : "+v"(to));
+                            const int k0 = 16 * (to >> 3) + 8 * hh + (to & 7);
+                            // (the symbol's base is wave-uniform when a wave holds one symbol)
+                            gptr<C> yg = TPS >= 64 ? uniform_ptr(ys) : (gptr<C>)ys;
+#pragma unroll
+                            for (int i = 0; i < 8; ++i)
+                                st_stream<TX_NT>(lane_ptr(yg, (uint32_t)(k0 + 2 * TPS * i)), crow[wfir_slot(to + TPS * i)]);
+                        }
+                    }
+                    if (live) {
                         if (t < cp) {
                             const R pr = pT - pU, pi = pT + pV;
                             pys = __builtin_fma(pr, pr, pys);

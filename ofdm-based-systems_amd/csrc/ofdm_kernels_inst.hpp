@@ -160,6 +160,8 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
         // window FIR row: stream samples [-(LT-1), N+cp) at fir_pad(R0 + m)
         const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
         a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
+        // complex128: the row of reals also carries N / 2 complex outputs (wfir_slot) per half
+        if (sizeof(R) == 8) a.slot = std::max(a.slot, 2 * (wfir_slot((1 << LOGN) / 2 - 1) + 1));
     }
     const size_t sm = smem_tx<R>(LOGN, BLK, FB > 0 ? 0 : a.c.lut_len, a.c.words_per_sym, a.L, a.slot,
                                  uses_tt<R, LOGN, FB>() ? tt_size(LOGN) : 0, FB > 0 && LT > 0,
