@@ -760,58 +760,72 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         row[fir_pad(R0 - (LT - 1) + t)] = z < 0 ? mk<R>(0, 0) : tl[z];
                     }
                     sym_sync<TPS>();
-                    if (sizeof(R) == 4 && active && c >= 0) {
-                        // taps (zero past L), LDS broadcast reads; the opaque offset keeps the reads
-                        // in the symbol loop (hoisted, the 4 LT registers stay live through the FFT
-                        // and spill)
-                        int ho = 0;
-                        asm volatile("" : "+v"(ho));
-                        f32x2 hv[LT], hs[LT];
+                    // complex64: taps (zero past L), LDS broadcast reads; the opaque offset keeps
+                    // the reads in the symbol loop (hoisted, the 4 LT registers stay live through
+                    // the FFT and spill)
+                    const bool live = active && c >= 0;
+                    int ho = 0;
+                    asm volatile("" : "+v"(ho));
+                    f32x2 hv[LT], hs[LT];
 #pragma unroll
-                        for (int q = 0; q < LT; ++q) {
-                            hv[q] = f32x2{(float)h[ho + q].re, (float)h[ho + q].im};
-                            hs[q] = f32x2{(float)hsw[ho + q].re, (float)hsw[ho + q].im};
+                    for (int q = 0; q < LT; ++q) {
+                        hv[q] = f32x2{(float)h[ho + q].re, (float)h[ho + q].im};
+                        hs[q] = f32x2{(float)hsw[ho + q].re, (float)hsw[ho + q].im};
+                    }
+                    // the window (every lane, live or not), the prefix-region output and the tail
+                    // leave the row first: the outputs take its place
+                    const C* wb = row + (A + (A >> 4) + 17 * t);
+                    f32x2 win[WN];
+#pragma unroll
+                    for (int w = 0; w < WN; ++w) {
+                        const C ev = wb[w + (w >> 4)];
+                        win[w] = f32x2{(float)ev.re, (float)ev.im};
+                    }
+                    R pys = 0;
+                    if (live && t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
+                        f32x2 yp = f32x2{0.f, 0.f};
+#pragma unroll
+                        for (int l = 0; l < LT; ++l) {
+                            const C ev = row[fir_pad(R0 + t - l)];
+                            const f32x2 e = f32x2{(float)ev.re, (float)ev.im};
+                            yp = __builtin_elementwise_fma(e.xx, hv[l], yp);
+                            yp = __builtin_elementwise_fma(e.yy, hs[l], yp);
                         }
-                        const C* wb = row + (A + (A >> 4) + 17 * t);
-                        f32x2 win[WN];
-#pragma unroll
-                        for (int w = 0; w < WN; ++w) {
-                            const C ev = wb[w + (w >> 4)];
-                            win[w] = f32x2{(float)ev.re, (float)ev.im};
-                        }
-                        f32x2 pacc = f32x2{0.f, 0.f};  // (sum Re^2, sum Im^2): one packed FMA per output
-                        float4* yo = (float4*)(yout + sl * N + E * t);
-#pragma unroll
-                        for (int j = 0; j < E; j += 2) {
-                            f32x2 y0 = f32x2{0.f, 0.f}, y1 = f32x2{0.f, 0.f};
-#pragma unroll
-                            for (int l = 0; l < LT; ++l) {
-                                const f32x2 e0 = win[j + LT - 1 - l], e1 = win[j + LT - l];
-                                y0 = __builtin_elementwise_fma(e0.xx, hv[l], y0);
-                                y0 = __builtin_elementwise_fma(e0.yy, hs[l], y0);
-                                y1 = __builtin_elementwise_fma(e1.xx, hv[l], y1);
-                                y1 = __builtin_elementwise_fma(e1.yy, hs[l], y1);
-                            }
-                            pacc = __builtin_elementwise_fma(y0, y0, pacc);
-                            pacc = __builtin_elementwise_fma(y1, y1, pacc);
-                            if (yout && !(flags & 4)) yo[j >> 1] = float4{y0.x, y0.y, y1.x, y1.y};
-                        }
-                        R pys = pacc.x + pacc.y;
-                        if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
-                            f32x2 yp = f32x2{0.f, 0.f};
-#pragma unroll
-                            for (int l = 0; l < LT; ++l) {
-                                const C ev = row[fir_pad(R0 + t - l)];
-                                const f32x2 e = f32x2{(float)ev.re, (float)ev.im};
-                                yp = __builtin_elementwise_fma(e.xx, hv[l], yp);
-                                yp = __builtin_elementwise_fma(e.yy, hs[l], yp);
-                            }
-                            pys += yp.x * yp.x + yp.y * yp.y;
-                        }
-                        fx_accum((double)pys, pq0, pq1);
+                        pys = yp.x * yp.x + yp.y * yp.y;
                     }
                     // tail for the next symbol: the last L-1 stream samples (zeros before symbol 0)
                     if (t < L - 1) tl[t] = active ? row[fir_pad(R0 + N + cp - (L - 1) + t)] : mk<R>(0, 0);
+                    sym_sync<TPS>();
+                    // the lane's 16 consecutive outputs k = 16 t + j go to row[fir_pad(k)] and
+                    // leave as k = t + TPS i: whole-line stores instead of 16 lines per lane
+                    f32x2 pacc = f32x2{0.f, 0.f};  // (sum Re^2, sum Im^2): one packed FMA per output
+#pragma unroll
+                    for (int j = 0; j < E; j += 2) {
+                        f32x2 y0 = f32x2{0.f, 0.f}, y1 = f32x2{0.f, 0.f};
+#pragma unroll
+                        for (int l = 0; l < LT; ++l) {
+                            const f32x2 e0 = win[j + LT - 1 - l], e1 = win[j + LT - l];
+                            y0 = __builtin_elementwise_fma(e0.xx, hv[l], y0);
+                            y0 = __builtin_elementwise_fma(e0.yy, hs[l], y0);
+                            y1 = __builtin_elementwise_fma(e1.xx, hv[l], y1);
+                            y1 = __builtin_elementwise_fma(e1.yy, hs[l], y1);
+                        }
+                        pacc = __builtin_elementwise_fma(y0, y0, pacc);
+                        pacc = __builtin_elementwise_fma(y1, y1, pacc);
+                        row[fir_pad(E * t + j)] = mk<R>(y0.x, y0.y);
+                        row[fir_pad(E * t + j + 1)] = mk<R>(y1.x, y1.y);
+                    }
+                    sym_sync<TPS>();
+                    if (live && yout && !(flags & 4)) {
+                        C* ys = yout + sl * N;
+                        int to = t;  // opaque: offsets hoisted out of the loop would hold registers
+                        asm volatile("" : "+v"(to));
+                        gptr<C> yg = TPS >= 64 ? uniform_ptr(ys) : (gptr<C>)ys;
+#pragma unroll
+                        for (int i = 0; i < E; ++i)
+                            st_stream<TX_NT>(lane_ptr(yg, (uint32_t)(to + TPS * i)), row[fir_pad(to + TPS * i)]);
+                    }
+                    if (live) fx_accum((double)(pys + pacc.x + pacc.y), pq0, pq1);
                     sym_sync<TPS>();
                 }
             } else {
