@@ -130,6 +130,17 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
     return (gptr<T>)((__attribute__((address_space(1))) char*)base + (uint64_t)(elem * (uint32_t)sizeof(T)));
 }
 
+// Raw buffer resource over `bytes` bytes at p (gfx9 word 3) and a 16-byte load at a lane byte
+// offset (VGPR) plus a wave-uniform one (SGPR): one address register for any number of loads.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+template <typename T>
+__device__ __forceinline__ T buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    static_assert(sizeof(T) == 16, "16-byte element");
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+
 // MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
 #ifndef OFDM_TX_MP_BLOCK
 #define OFDM_TX_MP_BLOCK 256
@@ -224,9 +235,24 @@ __host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
 #endif
 template <typename R, int FB, int LOGN>
 constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB > 1 && LOGN >= 6 && LOGN <= 10; }
+// complex128 RX of fixed QAM at N = 4096 (config e): one symbol per 256-thread workgroup at 3 waves
+// per SIMD, the equaliser coefficients read from the plan's table after the FFT (rx_eq_late)
+// instead of a 64 KB LDS copy per workgroup -- with the copy, two symbols per 512-thread workgroup
+// at 2 waves per SIMD, one barrier coupling both symbols' FFT exchanges.  Config e RX 5.02 ->
+// 4.21 ms per 2.5e5 symbols (2 waves per SIMD: 4.63); the step gains less (9.99 -> 9.64 ms): the
+// TX that follows runs 0.4 ms slower at the power cap (profiles/r03y_ab.txt)
+#ifndef OFDM_F64_RX_SOLO
+#define OFDM_F64_RX_SOLO 1
+#endif
+#ifndef OFDM_F64_RX_SOLO_WAVES
+#define OFDM_F64_RX_SOLO_WAVES 3
+#endif
+template <typename R, int FB, int LOGN>
+constexpr bool f64_rx_solo() { return OFDM_F64_RX_SOLO && sizeof(R) == 8 && FB > 1 && LOGN == 12; }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_block() {
     // (the adaptive kernel's per-order tables take ~200 VGPRs in complex128: 2 waves per SIMD)
+    if (f64_rx_solo<R, FB, LOGN>()) return 256;
     if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 512 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_BLOCK : 768);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_BLOCK(LOGN);
     return rx_prefetch<R, FB, LOGN>() ? kBlock
@@ -234,6 +260,7 @@ constexpr int rx_block() {
 }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_waves() {
+    if (f64_rx_solo<R, FB, LOGN>()) return OFDM_F64_RX_SOLO_WAVES;
     if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 2 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_WAVES : 3);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;
     return rx_prefetch<R, FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
@@ -250,8 +277,19 @@ constexpr int rx_waves() {
 // twiddles, and preloading 16 complex128 coefficients would spill
 template <typename R, int FB, int LOGN, int EQ>
 constexpr bool eq_in_lds() {
-    return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= (sizeof(R) == 8 ? 12 : OFDM_EQ_LDS_MAX_LOGN);
+    return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= (sizeof(R) == 8 ? 12 : OFDM_EQ_LDS_MAX_LOGN) &&
+           !f64_rx_solo<R, FB, LOGN>();
 }
+// the lane's coefficients loaded after the FFT (in flight across the MMSE power reduction)
+template <typename R, int FB, int LOGN, int EQ>
+constexpr bool rx_eq_late() { return f64_rx_solo<R, FB, LOGN>() && EQ > OFDM_EQ_NONE; }
+// MMSE in complex128: the reciprocals of |H|^2 + nv of four elements from one v_rcp_f64 (+ two
+// Newton steps) and nine products (Montgomery's batch inversion; ~3 roundings more than one
+// reciprocal each, well inside the decision bracket's 8 u of equaliser arithmetic).  RX c 3.80 ->
+// 3.75, e 4.21 -> 4.16 ms per step (profiles/r03y_ab.txt)
+#ifndef OFDM_MMSE_BATCH
+#define OFDM_MMSE_BATCH 1
+#endif
 // complex128 throughput kernels exchange FFT data through rows of reals (fft_reg_split)
 template <typename R, int FB>
 constexpr bool split_rows() { return sizeof(R) == 8 && FB > 0; }
@@ -944,8 +982,11 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     // otherwise (throughput kernels at N = 4096, and the complex64 generic kernel) the lane's
     // coefficients are loaded before the FFT each symbol (L2-resident), so their latency hides
     // behind it instead of stalling each element of the equaliser
+    constexpr bool EQ_LATE = rx_eq_late<R, FB, LOGN, EQ>();
     constexpr bool EQ_PRE =
-        OFDM_EQ_PRE && !EQ_LDS && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
+        OFDM_EQ_PRE && !EQ_LDS && !EQ_LATE && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
+    constexpr bool EQ_REG = EQ_PRE || EQ_LATE;  // coefficients in registers (ecoef)
+    constexpr bool MMSE_BATCH = OFDM_MMSE_BATCH && sizeof(R) == 8 && FB > 1 && EQ == OFDM_EQ_MMSE;
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     const bool noise = a.noise_on && !(flags & 1);
@@ -998,11 +1039,12 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     C* row = (C*)(rowmem + (size_t)ls * G::PADN * (SPLIT ? sizeof(R) : sizeof(C)));
     uint32_t* W = words + ls * cm.words_per_sym;
     const C* eqa = (const C*)cm.eq_a;
+    const __amdgpu_buffer_rsrc_t eq_rsrc = buf_rsrc(eqa, (uint32_t)(N * sizeof(C)));
     const R* eqb = (const R*)cm.eq_b;
     // ZF / MMSE of subcarrier k (equalization/models.py:22-63); nv: the symbol's MMSE noise variance
     // (pa: the coefficient the throughput kernel preloaded for this element, or null)
     auto eq_apply = [&](C v, int k, R nv, const C* pa) -> C {
-        if constexpr (EQ_LDS || EQ_PRE) {
+        if constexpr (EQ_LDS || EQ_REG) {
             // ZF 1/H; MMSE conj(H) with |H|^2 recomputed from it (complex64 only)
             const C c = EQ_LDS ? eqt[k] : *pa;
             if (eq == OFDM_EQ_ZF) return cmul(v, c);
@@ -1140,7 +1182,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
 #pragma unroll
             for (int i = 0; i < E; ++i) x[i] = cscale(x[i], scale);
         }
-        C ecoef[EQ_PRE ? E : 1];
+        C ecoef[EQ_REG ? E : 1];
         if constexpr (EQ_PRE) {
             if (eq != OFDM_EQ_NONE) {
 #pragma unroll
@@ -1148,6 +1190,18 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
             }
         }
         if (!(flags & 2)) fft_sym<R, LOGN, false, FB>(x, row, tw, tt, t);
+        // (late loads: the first four here, each later four one slicer group ahead)
+        // (buffer loads, the lane's byte offset + element i's in an SGPR: one address VGPR, where
+        // 16 hoisted 64-bit addresses spilled at 3 waves per SIMD)
+        auto load_coef4 = [&](int q) {
+            if constexpr (EQ_LATE) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    ecoef[4 * q + j] = buf_load16<C>(eq_rsrc, (uint32_t)t * (uint32_t)sizeof(C),
+                                                     (uint32_t)((4 * q + j) * TPS * (int)sizeof(C)));
+            }
+        };
+        if constexpr (EQ_LATE) load_coef4(0);
         if (FB == 0) sym_sync<TPS>();  // staged words visible to the whole group
         // MMSE noise variance per OFDM symbol (equalization/models.py:39-49)
         R nv = 0;
@@ -1171,7 +1225,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
 #pragma unroll
             for (int i = 0; i < E; ++i)
                 if (eq != OFDM_EQ_NONE)
-                    x[i] = eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_PRE ? i : 0]);
+                    x[i] = eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_REG ? i : 0]);
             sym_sync<TPS>();  // the forward FFT has read the row
             if constexpr (FB > 1) {
                 fft_sym<R, LOGN, true, FB>(x, row, tw, tt + TTS, t);  // 1/N in the slicer
@@ -1187,7 +1241,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
             uint32_t bes = 0, ses = 0;
             auto equalized = [&](int i) {
                 if (scm || eq == OFDM_EQ_NONE) return x[i];  // single carrier: equalised before the IFFT
-                return eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_PRE ? i : 0]);
+                return eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_REG ? i : 0]);
             };
             if constexpr (FB == 1) {
                 // four elements per lane word, each through its subcarrier's order (the codes
@@ -1231,9 +1285,36 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
                 // four elements per lane word: slice, look up, compare, count
                 static_for<0, E / 4>([&](auto Q) {
                     constexpr int q = Q;
+                    if constexpr (EQ_LATE && q + 1 < E / 4) load_coef4(q + 1);
                     C z[4];
+                    if constexpr (MMSE_BATCH) {
+                        // conj(H) v / (|H|^2 + nv) with the four reciprocals from one
+                        C c[4];
+                        R dn[4], inv[4];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
+                        for (int j = 0; j < 4; ++j) {
+                            c[j] = EQ_LDS ? eqt[t + (4 * q + j) * TPS] : ecoef[EQ_REG ? 4 * q + j : 0];
+                            dn[j] = c[j].re * c[j].re + c[j].im * c[j].im + nv;
+                        }
+                        const R p01 = dn[0] * dn[1], p012 = p01 * dn[2], p = p012 * dn[3];
+                        if (__builtin_expect(p >= (R)1e-280 && p <= (R)1e280, 1)) {
+                            R r = recip<R>(p);  // 1 / (d0 d1 d2 d3)
+                            inv[3] = r * p012;
+                            r *= dn[3];  // 1 / (d0 d1 d2)
+                            inv[2] = r * p01;
+                            r *= dn[2];  // 1 / (d0 d1)
+                            inv[1] = r * dn[0];
+                            inv[0] = r * dn[1];
+                        } else {  // a zero, infinite or extreme factor: one reciprocal each
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) inv[j] = recip<R>(dn[j]);
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) z[j] = cscale(cmul(x[4 * q + j], c[j]), inv[j]);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
+                    }
                     uint32_t d = 0;
                     // the reference's M-PSK (M <= 32: 4- and 16-PSK share the QAM kernels'
                     // FB = 2 / 4, 8- and 32-PSK have FB = 3 / 5 to themselves): sector
