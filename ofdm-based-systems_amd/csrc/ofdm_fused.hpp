@@ -135,11 +135,28 @@ __device__ __forceinline__ gptr<T> lane_ptr(gptr<T> base, uint32_t elem) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
-template <typename T>
+// (NT: the nontemporal hint, cache-policy bit 1 on gfx950)
+template <typename T, bool NT = false>
 __device__ __forceinline__ T buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     static_assert(sizeof(T) == 16, "16-byte element");
-    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+    return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, NT ? 2 : 0));
 }
+
+// complex128 multipath TX of square QAM (the plan sends only separable LUTs to the throughput
+// kernels): map through the two axis tables instead of the complex LUT (TX c 5.13 -> 5.12, e 5.26
+// -> 5.17 ms per step, profiles/r03aa_ab.txt)
+#ifndef OFDM_TX_SEP_LUT
+#define OFDM_TX_SEP_LUT 1
+#endif
+template <typename R, int FB, int LT>
+constexpr bool tx_sep_lut() { return OFDM_TX_SEP_LUT && sizeof(R) == 8 && FB >= 2 && !(FB & 1) && LT != 0; }
+
+// complex128 RX with a symbol per wave: the channel samples through buffer loads (one address
+// VGPR, the element offsets in SGPRs) instead of four 64-bit VGPR addresses (RX b 3.09 -> 3.06,
+// c 3.75 -> 3.70 ms per step at the same occupancy, profiles/r03ab_ab.txt)
+#ifndef OFDM_RX_BUF
+#define OFDM_RX_BUF 1
+#endif
 
 // MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
 #ifndef OFDM_TX_MP_BLOCK
@@ -150,7 +167,9 @@ __device__ __forceinline__ T buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 // registers: 16 complex128 elements per lane plus a radix-16 butterfly -- RX ~160 VGPRs (3 waves
 // per SIMD: one 768-thread workgroup of 12 symbols per CU), flat TX 128 (4 waves: 1024 threads).
 // A 4-wave RX (1024 threads, 128 VGPRs, 7 spilled) measured config b 1.646 -> 1.648e8 symbols/s,
-// within the run-to-run spread (profiles/r03k_ab_rx1024.txt): not taken.
+// within the run-to-run spread (profiles/r03k_ab_rx1024.txt); with the channel samples
+// buffer-loaded (OFDM_RX_BUF: 6 dwords spilled at 128) it gains: RX 3.09 -> 2.98 ms, 1.669 ->
+// 1.693e8 symbols/s (profiles/r03ab_ab.txt) -- the no-equaliser RX takes 1024 threads at 4 waves.
 // The window-FIR TX passes the extended stream through its row of reals twice (real, then
 // imaginary parts), in 256-thread workgroups at 2 waves per SIMD: two or more workgroups per
 // CU, so a symbol group's barriers (N >= 2048: TPS > 64) hold back fewer waves.  Against
@@ -164,10 +183,10 @@ __device__ __forceinline__ T buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 #define OFDM_F64_TX_WAVES 4
 #endif
 #ifndef OFDM_F64_RX_BLOCK
-#define OFDM_F64_RX_BLOCK 768
+#define OFDM_F64_RX_BLOCK 1024
 #endif
 #ifndef OFDM_F64_RX_WAVES
-#define OFDM_F64_RX_WAVES 3
+#define OFDM_F64_RX_WAVES 4
 #endif
 #ifndef OFDM_F64_FIR_BLOCK
 #define OFDM_F64_FIR_BLOCK 256
@@ -247,13 +266,18 @@ constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB >
 #ifndef OFDM_F64_RX_SOLO_WAVES
 #define OFDM_F64_RX_SOLO_WAVES 3
 #endif
+// the OFDM_F64_RX_BLOCK / _WAVES shape: no-equaliser RX of 64/256-QAM at N = 1024 (at 128 VGPRs the
+// QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves)
+template <int FB, int LOGN, int EQ>
+constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10; }
 template <typename R, int FB, int LOGN>
 constexpr bool f64_rx_solo() { return OFDM_F64_RX_SOLO && sizeof(R) == 8 && FB > 1 && LOGN == 12; }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_block() {
     // (the adaptive kernel's per-order tables take ~200 VGPRs in complex128: 2 waves per SIMD)
     if (f64_rx_solo<R, FB, LOGN>()) return 256;
-    if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 512 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_BLOCK : 768);
+    if (sizeof(R) == 8 && FB > 0)
+        return (LOGN > 10 || FB == 1) ? 512 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_BLOCK : 768);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_BLOCK(LOGN);
     return rx_prefetch<R, FB, LOGN>() ? kBlock
                                        : (FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock);
@@ -261,7 +285,7 @@ constexpr int rx_block() {
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_waves() {
     if (f64_rx_solo<R, FB, LOGN>()) return OFDM_F64_RX_SOLO_WAVES;
-    if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 2 : (EQ == OFDM_EQ_NONE ? OFDM_F64_RX_WAVES : 3);
+    if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 2 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_WAVES : 3);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;
     return rx_prefetch<R, FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
 }
@@ -494,6 +518,10 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     // generic kernel: dynamic
     constexpr int LUT_STATIC = FB == 1 ? kMaxLut + 1 : (FB > 1 ? (1 << FB) : 1);
     __shared__ C lut_s[LUT_STATIC];
+    // complex128 multipath TX of square QAM: the LUT as its two axis tables (tx_sep_lut)
+    constexpr bool SEP = tx_sep_lut<R, FB, LT>();
+    constexpr int HB = FB / 2, SIDE = 1 << HB;
+    __shared__ R sep_s[SEP ? 2 * SIDE : 1];
     C* lut = FB > 0 ? lut_s : cv.take<C>(cm.lut_len);
     C* h = cv.take<C>(32);
     C* hsw = cv.take<C>(WFIR ? 32 : 0);  // window FIR: the taps swizzled, (-im, re)
@@ -518,6 +546,14 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     const C hf = FOLD_H0 ? ((const C*)a.h)[0] : mk<R>(1, 0);
     for (int i = threadIdx.x; i < cm.lut_len; i += BLK)
         lut[i] = cscale(FOLD_H0 ? cmul(hf, ((const C*)cm.lut)[i]) : ((const C*)cm.lut)[i], lut_scale);
+    if constexpr (SEP) {
+        // LUT[i] = I[i & (SIDE - 1)] + j Q[i >> HB] exactly (the plan's build_axis verified it):
+        // I from the entries with Q index 0, Q from those with I index 0, the same scaled values
+        if (threadIdx.x < SIDE) {
+            sep_s[threadIdx.x] = ((const C*)cm.lut)[threadIdx.x].re * lut_scale;
+            sep_s[SIDE + threadIdx.x] = ((const C*)cm.lut)[threadIdx.x << HB].im * lut_scale;
+        }
+    }
     if constexpr (FB == 1) {
         if (threadIdx.x == 0) lut[cm.lut_len] = mk<R>(0, 0);
         for (int k = threadIdx.x; k < N; k += BLK) {
@@ -577,6 +613,13 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     const uint32_t e = sce[st + I * TPS];
                     const uint32_t v = (lane_word(tb.lane, I >> 2) >> (8 * (I & 3))) & e & 0xFFu;
                     x[I] = lut[(e >> 8) + v];
+                });
+            } else if constexpr (SEP) {
+                // two 8-byte reads from SIDE-entry tables: distinct entries sit on distinct banks
+                // (the 2^FB-entry complex table's random 16-byte reads conflicted)
+                static_for<0, E>([&](auto I) {
+                    const uint32_t v = tb.template fixed<I>();
+                    x[I] = mk<R>(sep_s[v & (SIDE - 1)], sep_s[SIDE + (v >> HB)]);
                 });
             } else if constexpr (FB > 0) {
                 static_for<0, E>([&](auto I) { x[I] = lut[tb.template fixed<I>()]; });
@@ -1094,9 +1137,22 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     // kept channel samples of local symbol sl.  Past the end the wave reads the last symbol
     // again (its results are neither counted nor stored): an unconditional load, where zeroing
     // the 16 elements cost 32 v_mov_b64 per symbol in complex128.  Zeros when ablated.
+    constexpr bool RX_BUF = OFDM_RX_BUF && F64_FAST && TPS == 64;
     auto load_sym = [&](int64_t sl, C (&dst)[E]) {
         const C* ys = (const C*)a.y + (sl < cm.n_sym ? sl : cm.n_sym - 1) * ystride;
-        if (!(flags & 16)) {
+        if (RX_BUF && !(flags & 16)) {
+            // complex128, a symbol per wave: buffer loads off the symbol's row, the lane's byte
+            // offset in one VGPR and element i's in the instruction's SGPR offset
+            if constexpr (RX_BUF) {
+                const __amdgpu_buffer_rsrc_t r = buf_rsrc(ys, (uint32_t)(N * sizeof(C)));
+#pragma unroll
+                for (int i = 0; i < E; ++i) {
+                    dst[i] = buf_load16<C, (bool)OFDM_RX_NT>(r, (uint32_t)t * (uint32_t)sizeof(C),
+                                                             (uint32_t)(i * TPS * (int)sizeof(C)));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        } else if (!(flags & 16)) {
             // issued in element order, the order the noise consumes them: each add then waits
             // for its own load only (left to the scheduler, the N = 4096 complex128 RX issued
             // element 0 thirteenth and waited for 13 of 16 loads before its first add)
