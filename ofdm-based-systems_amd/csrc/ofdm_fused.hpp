@@ -270,12 +270,21 @@ constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB >
 // QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves)
 template <int FB, int LOGN, int EQ>
 constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10; }
+// (OFDM_F64_RX_SOLO_D: the same for the adaptive RX at N = 2048 (config d) -- 128-thread workgroups
+// of one symbol at 2 waves per SIMD, instead of four symbols per 512-thread workgroup: RX 5.12 ->
+// 4.67 ms, step 10.11 -> 9.93 ms per 5e5 symbols, profiles/r03ad_ab.txt)
+#ifndef OFDM_F64_RX_SOLO_D
+#define OFDM_F64_RX_SOLO_D 1
+#endif
 template <typename R, int FB, int LOGN>
-constexpr bool f64_rx_solo() { return OFDM_F64_RX_SOLO && sizeof(R) == 8 && FB > 1 && LOGN == 12; }
+constexpr bool f64_rx_solo() {
+    return OFDM_F64_RX_SOLO && sizeof(R) == 8 &&
+           ((FB > 1 && LOGN == 12) || (OFDM_F64_RX_SOLO_D && FB == 1 && LOGN == 11));
+}
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_block() {
     // (the adaptive kernel's per-order tables take ~200 VGPRs in complex128: 2 waves per SIMD)
-    if (f64_rx_solo<R, FB, LOGN>()) return 256;
+    if (f64_rx_solo<R, FB, LOGN>()) return (1 << LOGN) / 16;  // one symbol
     if (sizeof(R) == 8 && FB > 0)
         return (LOGN > 10 || FB == 1) ? 512 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_BLOCK : 768);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_BLOCK(LOGN);
@@ -284,7 +293,7 @@ constexpr int rx_block() {
 }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_waves() {
-    if (f64_rx_solo<R, FB, LOGN>()) return OFDM_F64_RX_SOLO_WAVES;
+    if (f64_rx_solo<R, FB, LOGN>()) return FB == 1 ? 2 : OFDM_F64_RX_SOLO_WAVES;
     if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 2 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_WAVES : 3);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;
     return rx_prefetch<R, FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
@@ -1304,6 +1313,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
                 // are made opaque per symbol: the order-table reads stay inside the loop)
                 static_for<0, E / 4>([&](auto Q) {
                     constexpr int q = Q;
+                    if constexpr (EQ_LATE && q + 1 < E / 4) load_coef4(q + 1);
                     C z[4];
                     const OP* op[4];
                     uint32_t oc = ocode[q];
