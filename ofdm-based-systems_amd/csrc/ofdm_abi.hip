@@ -201,6 +201,14 @@ int psk_order(const double* lut, int m) {
     return m;
 }
 
+// Multipath TX: consecutive OFDM symbols per symbol group; the group's first symbol regenerates
+// its predecessor's tail (one extra bits + map + IFFT per group).  32 against 16: complex128 TX
+// c 5.15 -> 5.00, d 5.24 -> 5.04, e 5.19 -> 5.00 ms per step; 64 leaves a ragged last round of
+// workgroups and measured slower than 32 (profiles/r03ag_ab.txt)
+#ifndef OFDM_TX_CHUNK
+#define OFDM_TX_CHUNK 32
+#endif
+
 #if OFDM_ABLATION
 // Diagnostic ablation switches for timing studies (tools/ablate.py), compiled only into
 // OFDM_ABLATION builds: the product library has no environment-controlled work skipping.
@@ -725,7 +733,7 @@ int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int
     a.h = p->h.p;
     a.L = p->L;
     std::memcpy(a.gtap, p->gtap, sizeof a.gtap);
-    a.chunk = p->L > 1 ? 16 : 1;
+    a.chunk = p->L > 1 ? OFDM_TX_CHUNK : 1;
     a.slot = tx_slot(p->logn, p->cp, p->L);
     a.flags = OFDM_ENV_FLAGS("OFDM_ABLATE_TX");
     int grid = 0;  // chosen by the launcher with the kernel (<= kMaxGrid partial records)

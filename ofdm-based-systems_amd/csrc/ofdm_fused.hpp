@@ -191,6 +191,9 @@ constexpr bool tx_sep_lut() { return OFDM_TX_SEP_LUT && sizeof(R) == 8 && FB >= 
 #ifndef OFDM_F64_FIR_BLOCK
 #define OFDM_F64_FIR_BLOCK 256
 #endif
+#ifndef OFDM_F64_FIR_WAVES
+#define OFDM_F64_FIR_WAVES 2
+#endif
 // complex64 throughput kernels at N >= 2048 (configs d, e): workgroup and waves per SIMD of RX
 // and of the window-FIR TX (two or four waves per symbol).  With the compact twiddle tables the
 // LDS no longer caps a CU at two workgroups, so 3 waves per SIMD fit: config e RX 3.37 -> 2.84 ms
@@ -230,7 +233,7 @@ constexpr int tx_block() {
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 template <typename R, int FB, int LOGN, int LT>
 constexpr int tx_waves() {
-    if (sizeof(R) == 8 && FB > 0) return LT == 0 ? OFDM_F64_TX_WAVES : 2;
+    if (sizeof(R) == 8 && FB > 0) return LT == 0 ? OFDM_F64_TX_WAVES : OFDM_F64_FIR_WAVES;
     if (FB > 0 && LT > 0 && LOGN > 10) return OFDM_TX_BIG_WFIR_WAVES;
     return block_waves(tx_block<R, FB, LOGN, LT>(), FB > 0 && LT > 0 ? OFDM_TX_WFIR_WAVES : OFDM_TX_WAVES);
 }
