@@ -70,6 +70,16 @@ static int resident_grid(F fn, int blk, size_t smem) {
     return cached[key] = std::max(1, std::min(kMaxGrid, per_cu * cus));
 }
 
+// A grid-stride grid larger than the device holds at once, cut to whole rounds of resident
+// workgroups: 4096 workgroups of config e's RX (768 resident) ran 5 full rounds and a sixth a
+// third full, the last ~1/16 of the kernel on a third of the chip
+#ifndef OFDM_GRID_ROUND
+#define OFDM_GRID_ROUND 0
+#endif
+static inline int whole_rounds(int grid, int resident) {
+    return (resident > 0 && grid > resident) ? (grid / resident) * resident : grid;
+}
+
 template <typename R, int LOGN, int MODE>
 static hipError_t rows_one(const RowsArgs& a, hipStream_t s) {
     const size_t sm = smem_rows<R>(LOGN);
@@ -172,6 +182,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     const int64_t groups = (a.c.n_sym + a.chunk - 1) / a.chunk;
     *grid = clamp_grid((groups + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
     if (OFDM_PERSISTENT && FB > 0) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
+    if (OFDM_GRID_ROUND && FB > 0) *grid = whole_rounds(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
@@ -256,6 +267,7 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     if (e != hipSuccess) return e;
     *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
     if (rx_prefetch<R, FB, LOGN>() || (OFDM_PERSISTENT && FB > 0)) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
+    if (OFDM_GRID_ROUND && FB > 0) *grid = whole_rounds(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
