@@ -270,7 +270,8 @@ constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB >
 #define OFDM_F64_RX_SOLO_WAVES 3
 #endif
 // the OFDM_F64_RX_BLOCK / _WAVES shape: no-equaliser RX of 64/256-QAM at N = 1024 (at 128 VGPRs the
-// QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves)
+// QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves;
+// with an equaliser the 16 KB coefficient table beside 16 symbols' rows exceeds the LDS)
 template <int FB, int LOGN, int EQ>
 constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10; }
 // (OFDM_F64_RX_SOLO_D: the same for the adaptive RX at N = 2048 (config d) -- 128-thread workgroups
