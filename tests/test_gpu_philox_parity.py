@@ -55,6 +55,9 @@ CASES = [
     (64, 16, "severe_multipath", "MMSE", 2048, 18.0, B.OFDM_F64, {}),
     (2048, 16, "flat_fading", "NONE", 256, 14.0, B.OFDM_F64, {}),
     (4096, 256, "Lin-Phoong_P1", "MMSE", 96, 31.0, B.OFDM_F64, {}),
+    # N = 4096 with one symbol per workgroup: ZF through the late coefficient loads, and no equaliser
+    (4096, 16, "Lin-Phoong_P1", "ZF", 64, 16.0, B.OFDM_F64, {}),
+    (4096, 64, "flat_fading", "NONE", 64, 20.0, B.OFDM_F64, {}),
     (256, 16, "severe_multipath", "MMSE", 512, 16.0, B.OFDM_F64, {"cp": 2}),
     (512, 4, "default_multipath", "ZF", 512, 12.0, B.OFDM_F64, {"cp": 0}),
     # SURVEY 8(f) variants on the generic kernel
@@ -98,6 +101,7 @@ CASES = [
     (64, 0, "default_multipath", "MMSE", 4097, 18.0, B.OFDM_F32, {"adaptive": True}),
     # ... and on the complex128 adaptive throughput kernel (FB = 1, double per-order tables)
     (2048, 0, "Lin-Phoong_P1", "MMSE", 255, 20.0, B.OFDM_F64, {"adaptive": True}),
+    (2048, 0, "two_ray", "ZF", 129, 24.0, B.OFDM_F64, {"adaptive": True}),  # one symbol per workgroup, ZF
     (256, 0, "two_ray", "ZF", 1023, 30.0, B.OFDM_F64, {"adaptive": True}),
     (1024, 0, "severe_multipath", "ZF", 257, 24.0, B.OFDM_F64, {"adaptive": True}),
     # CAPACITY_BASED with the PSK base mapper (orders 2..32 and unused subcarriers at an aggressive
