@@ -4,7 +4,7 @@ For every SNR point of the sweep (config (c): 0..30 dB in 1 dB steps plus 0.25 d
 26..29 dB) this runs
 
 * the throughput path (Philox / MWC64X bits and Box-Muller noise generated in the complex64
-  kernels), ``--symbols`` OFDM symbols per point, and
+  kernels, or complex128 with ``--precision f64``), ``--symbols`` OFDM symbols per point, and
 * the reference-stream path (the reference's PCG64 bytes and legacy normals through the
   complex128 kernels -- bit-exact with the reference NumPy code, tests/test_gpu_parity.py),
   ``--ref-symbols`` OFDM symbols per point (host stream generation bounds it),
@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--config", default="c", choices=sorted(CONFIGS))
     ap.add_argument("--symbols", type=int, default=2_000_000, help="throughput-mode OFDM symbols per SNR point")
     ap.add_argument("--ref-symbols", type=int, default=12_000, help="reference-stream OFDM symbols per SNR point")
+    ap.add_argument("--precision", default="f32", choices=("f32", "f64"),
+                    help="arithmetic of the throughput-mode kernels (complex64 / complex128)")
     ap.add_argument("--ref-min-snr", type=float, default=20.0,
                     help="below this SNR the reference-stream path runs --ref-symbols/8 (errors are plentiful)")
     args = ap.parse_args()
@@ -79,6 +81,7 @@ def main():
 
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
+    PREC = B.OFDM_F32 if args.precision == "f32" else B.OFDM_F64
     N, M, ch, eq, grid = CONFIGS[args.config]
     grid = sorted(set(grid))
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
@@ -93,8 +96,8 @@ def main():
             from bench import make_engine
 
             cfg = (N, M, ch, 1.0, eq, snr, "")
-            return make_engine(cfg, B.OFDM_F32)[0], make_engine(cfg, B.OFDM_F64)[0]
-        return (LinkEngine(N, cp, h, EQ[eq], lut, None, B.OFDM_F32),
+            return make_engine(cfg, args.precision), make_engine(cfg, "f64")
+        return (LinkEngine(N, cp, h, EQ[eq], lut, None, PREC),
                 LinkEngine(N, cp, h, EQ[eq], lut, None, B.OFDM_F64))
 
     e32 = e64 = None
@@ -135,7 +138,7 @@ def main():
             if et > 0 and er > 0:
                 x["log10_ber_ratio"] = math.log10(x["throughput"]["ber"] / x["reference_streams"]["ber"])
                 x["log10_ber_ratio_sigma"] = 0.4343 * math.sqrt(1.0 / et + 1.0 / er)
-        out = {"config": args.config, "n_fft": N, "qam_order": M, "channel": ch, "cp": cp, "equalizer": eq,
+        out = {"config": args.config, "throughput_precision": args.precision, "n_fft": N, "qam_order": M, "channel": ch, "cp": cp, "equalizer": eq,
                "n_gpus": world, "wall_s": time.perf_counter() - t0,
                "ber_1e-4_crossing_db": {"throughput": c_phx, "reference_streams": c_ref},
                "delta_db_at_1e-4": None if c_phx is None or c_ref is None else c_phx - c_ref,
