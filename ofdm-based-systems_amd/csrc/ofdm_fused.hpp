@@ -703,15 +703,15 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     if (zp && yout)
                         for (int j = t; j < cp; j += TPS) yo[N + j] = mk<R>(0, 0);
                     if constexpr (FOLD_H0) {
-                        fx_accum((double)pxs, pq0, pq1);  // the statistics above were taken on y (x |h0|^2 fixed below)
+                        fx_accum((R)pxs, pq0, pq1);  // the statistics above were taken on y (x |h0|^2 fixed below)
                     } else if constexpr (FB > 0) {
-                        fx_accum((double)(norm2(h0) * pxs), pq0, pq1);  // |y|^2 = |h0|^2 |x|^2 (complex64 mode)
+                        fx_accum((R)(norm2(h0) * pxs), pq0, pq1);  // |y|^2 = |h0|^2 |x|^2 (complex64 mode)
                     } else {
                         R pys = 0;
 #pragma unroll
                         for (int i = 0; i < E; ++i) pys += norm2(cmul(h0, x[i]));
                         pys += prefix_sum([&](int i) { return norm2(cmul(h0, x[i])); });
-                        fx_accum((double)pys, pq0, pq1);
+                        fx_accum((R)pys, pq0, pq1);
                     }
                 }
                 sym_sync<TPS>();  // W / row reuse by the next symbol
@@ -837,7 +837,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             pys = __builtin_fma(pr, pr, pys);
                             pys = __builtin_fma(pi, pi, pys);
                         }
-                        fx_accum((double)pys, pq0, pq1);
+                        fx_accum((R)pys, pq0, pq1);
                     }
                     sym_sync<TPS>();
                 } else {
@@ -919,7 +919,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         for (int i = 0; i < E; ++i)
                             st_stream<TX_NT>(lane_ptr(yg, (uint32_t)(to + TPS * i)), row[fir_pad(to + TPS * i)]);
                     }
-                    if (live) fx_accum((double)(pys + pacc.x + pacc.y), pq0, pq1);
+                    if (live) fx_accum((R)(pys + pacc.x + pacc.y), pq0, pq1);
                     sym_sync<TPS>();
                 }
             } else {
@@ -958,7 +958,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                                 yout[sl * N + (m - cp)] = yv;
                         }
                     }
-                    fx_accum((double)pys, pq0, pq1);
+                    fx_accum((R)pys, pq0, pq1);
                 }
                 // tail for the next symbol: the last L-1 stream samples (zeros before symbol 0)
                 for (int j = t; j < L - 1; j += TPS) tl[j] = active ? row[N + cp + j] : mk<R>(0, 0);
