@@ -92,70 +92,103 @@ def kernel_bytes_per_symbol(N: int, bps: int, cp: int, w: int = 8) -> int:
 
 
 # ---------------------------------------------------------------------------- CPU baseline
-def host_cores() -> int:
-    """CPUs this process may use: its affinity set, capped by the cgroup CPU quota when one is
-    set (on the GPU box os.cpu_count() and the affinity set report every CPU of the machine,
-    while the job's share is a quota)."""
+def host_cpus():
+    """(affinity-set size, cgroup CPU quota or None): on the GPU box os.cpu_count() and the
+    affinity set report every CPU of the machine, while the job's share is the cgroup quota."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
-        n = os.cpu_count() or 1
+        aff = os.cpu_count() or 1
+    quota = None
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
-            quota, period = f.read().split()[:2]
-        if quota != "max":
-            n = min(n, max(1, int(int(quota) / int(period))))
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
     except (OSError, ValueError):
         pass
-    return n
+    return aff, quota
 
 
-def _cpu_worker(args):
+def host_cores() -> int:
+    """CPUs this process may use: min(affinity set, cgroup quota)."""
+    aff, quota = host_cpus()
+    return min(aff, quota) if quota else aff
+
+
+def _cpu_worker(job, barrier, results):
+    """One CPU worker: imports and set-up first, then a shared barrier, then the timed sample --
+    the oracle run over `S` OFDM symbols in chunks (each chunk a complete run with its own
+    reference streams, so memory stays bounded), stream generation included as the GPU leg
+    generates its streams."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ofdm_oracle as O
 
-    seed, S, N, M, ch, cp, eq, snr = args
+    idx, seed, S, chunk, N, M, ch, cp, eq, snr = job
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
-    t0 = time.perf_counter()  # stream generation included, as the GPU leg generates its streams
+    orders = bps = None
     if M == 0:  # CAPACITY_BASED: orders from water-filling, the adaptive data path
         orders, _, _ = O.adaptive_orders(N, h, snr, 1e-3, True)
         bps = int(sum(int(np.log2(o)) for o in orders if o > 0))
-        tx, nz = O.reference_streams(seed, S * bps, S * (N + cp))
-        O.run_adaptive(tx, orders, N, h, cp, eq, snr, nz)
-    else:
-        b = int(np.log2(M))
-        tx, nz = O.reference_streams(seed, S * N * b, S * (N + cp))
-        O.run_fixed(tx, S * N * b, N, M, h, cp, eq, snr, nz)
-    return S, time.perf_counter() - t0
+    barrier.wait()
+    t0 = time.perf_counter()
+    done = 0
+    while done < S:
+        n = min(chunk, S - done)
+        if M == 0:
+            tx, nz = O.reference_streams(seed + done, n * bps, n * (N + cp))
+            O.run_adaptive(tx, orders, N, h, cp, eq, snr, nz)
+        else:
+            b = int(np.log2(M))
+            tx, nz = O.reference_streams(seed + done, n * N * b, n * (N + cp))
+            O.run_fixed(tx, n * N * b, N, M, h, cp, eq, snr, nz)
+        done += n
+    results.put((idx, S, t0, time.perf_counter()))
 
 
 def cpu_baseline(cfg, per_worker: int):
     """The NumPy oracle (a port of the reference path, complex128 like the reference) on every
-    CPU of this process, one worker per core, bounded sample."""
+    CPU of this process's share, one worker process per core, bounded sample.  The workers start,
+    import and set up, then meet at a barrier; each times its own sample from there, and value =
+    all symbols / the slowest worker's compute time (process start-up is reported beside it as
+    wall_incl_spawn_s, never in value)."""
     import multiprocessing as mp
 
     N, M, ch, ratio, eq, snr, _ = cfg
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
     cp = int(ratio * (len(h) - 1))
+    chunk = max(8, 2000 * 1024 // N)
     if M == 0:  # whole-byte runs: the adaptive decode needs S * sum(b_k) % 8 == 0
         per_worker = 8 * math.ceil(per_worker / 8)
+        chunk = 8 * math.ceil(chunk / 8)
+    aff, quota = host_cpus()
     workers = host_cores()
-    jobs = [(100 + i, per_worker, N, M, ch, cp, eq, snr) for i in range(workers)]
     ctx = mp.get_context("spawn")
-    t0 = time.perf_counter()
-    with ctx.Pool(workers) as pool:
-        out = pool.map(_cpu_worker, jobs)
-    wall = time.perf_counter() - t0
-    syms = sum(o[0] for o in out)
-    cpu_s = sum(o[1] for o in out)
+    barrier, results = ctx.Barrier(workers + 1), ctx.Queue()
+    w0 = time.perf_counter()
+    procs = [ctx.Process(target=_cpu_worker, args=((i, 100 + 7919 * i, per_worker, chunk, N, M, ch, cp, eq, snr),
+                                                   barrier, results)) for i in range(workers)]
+    for p in procs:
+        p.start()
+    barrier.wait()
+    out = [results.get() for _ in procs]
+    for p in procs:
+        p.join()
+    wall = time.perf_counter() - w0
+    syms = sum(o[1] for o in out)
+    durs = [o[3] - o[2] for o in out]
+    slowest = max(durs)
     return {
-        "value": syms / wall, "unit": "OFDM symbols/s", "cores": workers, "kind": "port",
-        "host_cpu_count": os.cpu_count(),
-        "sample": f"{workers} processes (one per CPU of this process's affinity set; the machine reports "
-                  f"{os.cpu_count()}) x {per_worker} OFDM symbols of the same config through the NumPy oracle in "
-                  f"complex128, reference PCG64 bits + legacy-normal noise generated inside the timing; "
-                  f"{cpu_s:.1f} s of CPU work, {wall:.1f} s wall incl. process start",
-        "per_core_symbols_per_s": syms / cpu_s,
+        "value": syms / slowest, "unit": "OFDM symbols/s", "cores": workers, "kind": "port",
+        "affinity_cpus": aff, "cgroup_quota_cpus": quota, "host_cpu_count": os.cpu_count(),
+        "sample": f"{workers} worker processes (min(affinity set {aff}, cgroup quota {quota}) CPUs; the machine "
+                  f"reports {os.cpu_count()}) x {per_worker} OFDM symbols of the same config through the NumPy "
+                  f"oracle in complex128, in runs of {chunk} symbols with the reference's PCG64 bits + legacy-normal "
+                  f"noise generated inside the timing; clock started per worker after a shared barrier (start-up "
+                  f"excluded), value = all symbols / slowest worker ({slowest:.1f} s; fastest {min(durs):.1f} s)",
+        "per_core_symbols_per_s": syms / sum(durs),
+        "slowest_worker_s": slowest,
+        "wall_incl_spawn_s": wall,
     }
 
 
@@ -377,7 +410,7 @@ def main():
                     help="arithmetic of the headline line (f64 = complex128, the reference's)")
     ap.add_argument("--no-variant", action="store_true", help="skip the complex64 companion run")
     ap.add_argument("--cpu-sample", type=int, default=0,
-                    help="OFDM symbols per CPU worker (default 1500 x 1024/N)")
+                    help="OFDM symbols per CPU worker (default 30000 x 1024/N: ~15 s of work per core)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ber-check", action="store_true", help="skip the BER Delta-dB check vs the reference streams")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
@@ -444,7 +477,7 @@ def main():
         out["ber_vs_reference"] = ber_vs_reference(eng64, N, engine.cp, snr, head["ber"], head["bits"],
                                                    symbols=max(2000, 16000 * 1024 // N))
     if rt.rank == 0 and rt.world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or max(100, 1500 * 1024 // N))
+        out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
     if rt.rank == 0:
         print(json.dumps(out), flush=True)
     rt.finish()

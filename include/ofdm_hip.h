@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define OFDM_ABI_VERSION 3
+#define OFDM_ABI_VERSION 4
 
 #define OFDM_OK 0
 #define OFDM_E_INVALID (-1)  /* bad argument / unsupported shape          */
@@ -158,6 +158,15 @@ int ofdm_demap_count(ofdm_plan_t plan, void* stream, const void* Z, const uint8_
    complex128 points: idx[i] = argmin_m |z_i - lut_m| (first on ties).  z is complex128. */
 int ofdm_nn_classify(void* stream, const double* lut, int32_t m, const void* z, int64_t n,
                      int64_t* idx);
+
+/* Throughput-mode noise radius (ABI 4): radius[i] = sqrt(32 - log2(float(words[i] | 0x1F8))),
+   evaluated exactly as the fused receivers evaluate it for every lane word (the float32 hardware
+   log2 / square root: the one step of the stream definition, csrc/ofdm_device.hpp noise_radius,
+   that IEEE arithmetic does not pin).  AWGNoiseModel.add_noise's Gaussian (noise/models.py:19-21)
+   in throughput mode is sigma sqrt(2 ln 2) radius (cos, sin)(phase); the checker
+   (oracle/philox_streams.py) takes these radii to restate the receivers' noise bit for bit.
+   words: device uint32 [n]; radius: device float [n]. */
+int ofdm_noise_radius(void* stream, const uint32_t* words, int64_t n, float* radius);
 
 /* OFDMModulator.modulate (modulation/models.py:27-39): x[s] = [cp | ifft(X[s], ortho)]
    (zero padding: [ifft(X[s], ortho) | 0...0]), X is (n_sym, N), x is (n_sym, N+cp). */

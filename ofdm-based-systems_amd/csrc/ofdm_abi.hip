@@ -625,6 +625,12 @@ int ofdm_nn_classify(void* stream, const double* lut, int32_t m, const void* z, 
     return OFDM_OK;
 }
 
+int ofdm_noise_radius(void* stream, const uint32_t* words, int64_t n, float* radius) {
+    if (n < 0 || (n > 0 && (!words || !radius))) return fail(OFDM_E_INVALID, "bad argument to ofdm_noise_radius");
+    HIPCHK(launch_noise_radius(words, n, radius, (hipStream_t)stream));
+    return OFDM_OK;
+}
+
 // The stream's partial-sum workspace (allocated on first use), or nullptr.
 static double* workspace(ofdm_plan_t p, void* stream) {
     std::lock_guard<std::mutex> lk(p->ws_mu);

@@ -919,12 +919,14 @@ __device__ __forceinline__ void fx_accum(double p, unsigned long long& l0, unsig
     const double a = p * 256.0;  // exact
     const double hi = floor(a);
     l1 += (unsigned long long)(uint32_t)hi;
-    l0 += (unsigned long long)(uint32_t)rint((a - hi) * 4294967296.0);  // (a - hi) exact; <= 2^32
+    // (a - hi) exact; its rounded multiple of 2^-40 can be exactly 2^32 (a fraction within 2^-41 of
+    // 1), so it is converted through 64 bits: the carry reaches l1 in fx_normalize
+    l0 += (unsigned long long)rint((a - hi) * 4294967296.0);
 }
 // complex64: the same limbs from a float32 share in float32 arithmetic.  Every step is exact:
 // p 2^8, its floor and its fraction are floats (Sterbenz), the fraction times 2^32 is a float below
 // 2^32, and only when p < 2^-17 does it carry bits below 2^0, which v_rndne_f32 rounds as rint does
-// in double -- so the limbs equal those of the double path (tests/test_oracle_philox.py restates
+// in double -- so the limbs equal those of the double path (tests/test_fixed_point.py restates
 // both), at ~10 full-rate VALU instead of ~10 f64 operations and conversions per lane and symbol.
 __device__ __forceinline__ void fx_accum(float p, unsigned long long& l0, unsigned long long& l1) {
     const float a = p * 256.0f;

@@ -36,12 +36,6 @@
 #ifndef OFDM_RX_WAVES
 #define OFDM_RX_WAVES 1
 #endif
-// RX order of the per-symbol prologue: 0 = Philox, loads, noise added element by element as the
-// loads land; 1 = loads, Philox, the whole noise into registers, then the adds; 2 = loads,
-// Philox, noise added element by element
-#ifndef OFDM_RX_NOISE_FIRST
-#define OFDM_RX_NOISE_FIRST 0
-#endif
 // Workgroup of the throughput (FB > 0) kernels at N <= 1024 (TX; RX without equaliser):
 // 8 waves share one copy of the twiddle tables and two workgroups fit the 160 KB LDS, i.e.
 // 4 waves per SIMD (register budget 128).  Other variants: 256 threads, OFDM_*_WAVES.
@@ -242,21 +236,6 @@ __host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
 // complex128 window-FIR TX: slot of output kk (of N / 2) in the row while it is transposed
 // for the store: one pad slot per 8, so the lanes' stride-8 writes fall on distinct banks
 __host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
-// Throughput RX (FB > 1, N <= 1024) software-pipelines its HBM loads: while a wave works on
-// one symbol, the channel samples of its next symbol are already in flight into registers
-// (E more VGPR pairs), so the load latency overlaps the FFT / noise / slicer instead of
-// waiting on a wave switch.  256-thread workgroups at OFDM_RX_PF_WAVES waves per SIMD.
-// Off: measured slower on MI355X (config b RX 1.90 -> 2.16 ms, c 2.72 -> 3.52 ms per 1e6
-// symbols at 3 waves/SIMD) -- the chip runs at its 1400 W power cap, so the overlap buys no
-// issue slots and the lower occupancy costs latency hiding in the FFT's LDS transposes.
-#ifndef OFDM_RX_PREFETCH
-#define OFDM_RX_PREFETCH 0
-#endif
-#ifndef OFDM_RX_PF_WAVES
-#define OFDM_RX_PF_WAVES 3
-#endif
-template <typename R, int FB, int LOGN>
-constexpr bool rx_prefetch() { return OFDM_RX_PREFETCH && sizeof(R) == 4 && FB > 1 && LOGN >= 6 && LOGN <= 10; }
 // complex128 RX of fixed QAM at N = 4096 (config e): one symbol per 256-thread workgroup at 3 waves
 // per SIMD, the equaliser coefficients read from the plan's table after the FFT (rx_eq_late)
 // instead of a 64 KB LDS copy per workgroup -- with the copy, two symbols per 512-thread workgroup
@@ -292,15 +271,14 @@ constexpr int rx_block() {
     if (sizeof(R) == 8 && FB > 0)
         return (LOGN > 10 || FB == 1) ? 512 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_BLOCK : 768);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_BLOCK(LOGN);
-    return rx_prefetch<R, FB, LOGN>() ? kBlock
-                                       : (FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock);
+    return FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock;
 }
 template <typename R, int FB, int LOGN, int EQ>
 constexpr int rx_waves() {
     if (f64_rx_solo<R, FB, LOGN>()) return FB == 1 ? 2 : OFDM_F64_RX_SOLO_WAVES;
     if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 2 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_WAVES : 3);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;
-    return rx_prefetch<R, FB, LOGN>() ? OFDM_RX_PF_WAVES : (rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES);
+    return rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES;
 }
 // throughput RX: equaliser coefficients staged in LDS up to N = 2^OFDM_EQ_LDS_MAX_LOGN (beyond,
 // the table would cost a resident workgroup per CU)
@@ -1179,10 +1157,6 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
             for (int i = 0; i < E; ++i) dst[i] = mk<R>(0, 0);
         }
     };
-    constexpr bool PF = rx_prefetch<R, FB, LOGN>();
-    C xn[PF ? E : 1];  // prefetched samples of the wave's next symbol
-    if constexpr (PF) load_sym((int64_t)blockIdx.x * G::SPB + ls, xn);
-
     for (int64_t it = blockIdx.x; it < niter; it += gridDim.x) {
         const int64_t sl = it * G::SPB + ls;
         const int64_t sg = cm.sym0 + sl;
@@ -1191,22 +1165,9 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
         // kept channel samples + AWGN; the 1/sqrt(N) of fft(norm="ortho") folded in
         const C* ys = (const C*)a.y + sl * ystride;
         C x[E];
-        if constexpr (PF) {
-#pragma unroll
-            for (int i = 0; i < E; ++i) x[i] = xn[i];
-            load_sym(sl + (int64_t)gridDim.x * G::SPB, xn);  // in flight during this symbol
-        }
-        if (!OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(flags & 4) || (noise && !array_noise)));
-        if constexpr (!PF) load_sym(sl, x);
-        if (OFDM_RX_NOISE_FIRST) tb.load(cm, sg, t, W, active && (!(flags & 4) || (noise && !array_noise)));
-        if (OFDM_RX_NOISE_FIRST == 1 && sizeof(R) == 4 && active && noise && !array_noise) {
-            // the lane's noise while the loads are in flight, then one add per element
-            f32x2 nz[E];
-#pragma unroll
-            for (int i = 0; i < E; ++i) nz[i] = tb.g.noise(ntab);
-#pragma unroll
-            for (int i = 0; i < E; ++i) x[i] = x[i] + mk<R>(nz[i].x, nz[i].y);
-        } else if (active && array_noise) {
+        tb.load(cm, sg, t, W, active && (!(flags & 4) || (noise && !array_noise)));
+        load_sym(sl, x);
+        if (active && array_noise) {
             const double* nr = a.nr + sg * (N + cp) + (zp ? 0 : cp);
             const double* ni = a.ni + sg * (N + cp) + (zp ? 0 : cp);
 #pragma unroll

@@ -427,6 +427,14 @@ __global__ __launch_bounds__(kBlock) void k_nn_classify(const double* lut, int m
         idx[e] = nn_index(z[2 * e], z[2 * e + 1], lut, m);
 }
 
+// The throughput-mode noise radius of each word (noise_radius: the fused receivers' float32
+// hardware log2 / sqrt, the one operation of the stream definition that is not IEEE-specified),
+// for the checker (ofdm_noise_radius).
+__global__ __launch_bounds__(kBlock) void k_noise_radius(const uint32_t* w, int64_t n, float* r) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += stride) r[e] = noise_radius(w[e]);
+}
+
 #endif  // OFDM_SUPPORT_KERNELS
 
 }  // namespace ofdm

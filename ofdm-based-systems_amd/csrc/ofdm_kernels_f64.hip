@@ -28,4 +28,11 @@ hipError_t launch_nn_classify(const double* lut, int m, const double* z, int64_t
                        lut, m, z, n, idx);
     return hipGetLastError();
 }
+
+hipError_t launch_noise_radius(const uint32_t* w, int64_t n, float* r, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    (void)hipGetLastError();  // stale errors were reported by their own calls
+    hipLaunchKernelGGL(k_noise_radius, dim3(clamp_grid((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, w, n, r);
+    return hipGetLastError();
+}
 }  // namespace ofdm

@@ -4,9 +4,6 @@
 #pragma once
 
 #include <algorithm>
-#include <map>
-#include <mutex>
-#include <tuple>
 
 #include "ofdm_kernels.hpp"
 
@@ -41,43 +38,6 @@ constexpr int kFastMinLogN = 6;  // throughput specialisations for N >= 64
 
 static inline int clamp_grid(int64_t want) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, kMaxGrid));
-}
-
-#ifndef OFDM_PERSISTENT
-#define OFDM_PERSISTENT 0
-#endif
-// Persistent grid for a grid-stride kernel: as many workgroups as the device holds at once
-// (occupancy x CUs), so no partial last round of workgroups idles part of the chip.  Cached per
-// kernel (its address: every instantiation has the same function type), device, workgroup size
-// and dynamic LDS.
-template <typename F>
-static int resident_grid(F fn, int blk, size_t smem) {
-    static std::mutex mu;
-    static std::map<std::tuple<const void*, int, int, size_t>, int> cached;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    const auto key = std::make_tuple(reinterpret_cast<const void*>(fn), dev, blk, smem);
-    std::lock_guard<std::mutex> lock(mu);
-    const auto it = cached.find(key);
-    if (it != cached.end()) return it->second;
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), blk, smem) !=
-            hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-        (void)hipGetLastError();
-        return kMaxGrid;
-    }
-    return cached[key] = std::max(1, std::min(kMaxGrid, per_cu * cus));
-}
-
-// A grid-stride grid larger than the device holds at once, cut to whole rounds of resident
-// workgroups: 4096 workgroups of config e's RX (768 resident) ran 5 full rounds and a sixth a
-// third full, the last ~1/16 of the kernel on a third of the chip
-#ifndef OFDM_GRID_ROUND
-#define OFDM_GRID_ROUND 0
-#endif
-static inline int whole_rounds(int grid, int resident) {
-    return (resident > 0 && grid > resident) ? (grid / resident) * resident : grid;
 }
 
 template <typename R, int LOGN, int MODE>
@@ -181,8 +141,6 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     if (e != hipSuccess) return e;
     const int64_t groups = (a.c.n_sym + a.chunk - 1) / a.chunk;
     *grid = clamp_grid((groups + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
-    if (OFDM_PERSISTENT && FB > 0) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
-    if (OFDM_GRID_ROUND && FB > 0) *grid = whole_rounds(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
@@ -266,8 +224,6 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
-    if (rx_prefetch<R, FB, LOGN>() || (OFDM_PERSISTENT && FB > 0)) *grid = std::min(*grid, resident_grid(fn, BLK, sm));
-    if (OFDM_GRID_ROUND && FB > 0) *grid = whole_rounds(*grid, resident_grid(fn, BLK, sm));
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }

@@ -242,5 +242,6 @@ hipError_t launch_finalize(const double* partials, int nblocks, int nfields, int
 hipError_t launch_finalize_tx(const double* partials, int nblocks, double* stats, hipStream_t s);
 hipError_t launch_nn_classify(const double* lut, int m, const double* z, int64_t n, int64_t* idx,
                               hipStream_t s);
+hipError_t launch_noise_radius(const uint32_t* w, int64_t n, float* r, hipStream_t s);
 
 }  // namespace ofdm

@@ -24,7 +24,7 @@ import torch
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
                          "libofdm_hip%s.so" % ("_" + os.environ["OFDM_LIB_VARIANT"]
                                                if os.environ.get("OFDM_LIB_VARIANT") else ""))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 OFDM_F32, OFDM_F64 = 0, 1
 # ofdm_stats (include/ofdm_hip.h): power_sum, x_power_sum, x_peak (double), power_fx[2] (int64)
@@ -92,6 +92,7 @@ SIGNATURES = {
     "ofdm_demap": (ctypes.c_int, [_VP, _VP, _VP, _I64, _VP]),
     "ofdm_demap_count": (ctypes.c_int, [_VP, _VP, _VP, _VP, _I64, _VP]),
     "ofdm_nn_classify": (ctypes.c_int, [_VP, _VP, _I32, _VP, _I64, _VP]),
+    "ofdm_noise_radius": (ctypes.c_int, [_VP, _VP, _I64, _VP]),
     "ofdm_modulate": (ctypes.c_int, [_VP, _VP, _VP, _I64, _VP]),
     "ofdm_demodulate": (ctypes.c_int, [_VP, _VP, _VP, _I64, _F64, _VP]),
     "ofdm_equalize": (ctypes.c_int, [_VP, _VP, _VP, _I64, _F64, _VP]),

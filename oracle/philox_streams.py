@@ -123,25 +123,39 @@ def noise_table(sigma: float) -> np.ndarray:
     return re.astype(np.float64) + 1j * im.astype(np.float64)
 
 
-def noise_from_words(w: np.ndarray, sigma: float, with_bound: bool = False):
+def noise_from_words(w: np.ndarray, sigma: float, with_bound: bool = False, radius_fn=None,
+                     product_rel: float = 2.0 ** -24):
     """Complex normal of each 32-bit lane word (radius from the word with bits 3..8 set,
     phase = bits 3..8 through the table).
 
-    with_bound: also return a bound on |GPU noise - this value| per word.  The GPU evaluates
-    log2 and sqrt with the float32 hardware instructions: log2 within 2 ulp of its float32 result
-    (<= 2^-18 absolute for arguments < 2^32), the subtraction from 32 and the square root within
-    1 ulp, the product with the table entry within 1/2 ulp per component.  With A = 32 - log2(f)
-    and dA = 2^-18 + 2^-23 A, the radius error is at most min(dA / sqrt(A), sqrt(dA)) + 2^-23 r."""
+    radius_fn: None -> the radius sqrt(32 - log2(f)) in float64 from the word's float32 value f;
+    otherwise a function mapping the words to the float32 radii the GPU's hardware log2 / sqrt
+    give (libofdm_hip's ofdm_noise_radius: the receivers' own noise_radius on these words).
+
+    with_bound: also return a bound on |GPU noise - this value| per word.
+    * float64 radius: the GPU evaluates log2 and sqrt with the float32 hardware instructions: log2
+      within 2 ulp of its float32 result (<= 2^-18 absolute for arguments < 2^32), the subtraction
+      from 32 and the square root within 1 ulp, the product with the table entry within 1/2 ulp per
+      component.  With A = 32 - log2(f) and dA = 2^-18 + 2^-23 A, the radius error is at most
+      dA / (sqrt(A) + sqrt(max(A - dA, 0))) (<= sqrt(dA)) + 2^-23 r.
+    * the GPU's radii: the float32 radius times the float32 table entry is exact in float64, as it
+      is in the complex128 receivers' fused multiply-add (product_rel 2^-53); the complex64
+      receivers round it once (product_rel 2^-24).  The table is the GPU's bit for bit when sigma is (float32 entries
+      of the same double sigma, tests/test_oracle_philox.py::test_noise_table_entries_are_robust)."""
     w = np.asarray(w, np.uint32)
+    e = noise_table(sigma)[(w >> np.uint32(3)) & np.uint32(NOISE_PHASES - 1)]
+    if radius_fn is not None:
+        r = np.asarray(radius_fn(w), np.float32).astype(np.float64)
+        n = r * e
+        return (n, product_rel * np.abs(n)) if with_bound else n
     f = (w | NOISE_MASK).astype(np.float32)  # round to nearest even, as v_cvt_f32_u32
     A = 32.0 - np.log2(f.astype(np.float64))
     r = np.sqrt(A)
-    e = noise_table(sigma)[(w >> np.uint32(3)) & np.uint32(NOISE_PHASES - 1)]
     n = r * e
     if not with_bound:
         return n
     dA = 2.0 ** -18 + 2.0 ** -23 * A
-    dr = np.minimum(dA / np.maximum(np.sqrt(A), 1e-300), np.sqrt(dA)) + 2.0 ** -23 * r
+    dr = dA / np.maximum(np.sqrt(A) + np.sqrt(np.maximum(A - dA, 0.0)), np.sqrt(dA)) + 2.0 ** -23 * r
     return n, dr * np.abs(e) + 2.0 ** -23 * np.abs(n)
 
 
@@ -162,11 +176,12 @@ def tx_indices(gen: LaneStream, S: int, N: int, b) -> np.ndarray:
     return _lane_to_row(byte.astype(np.int64), S, N) & mask[None, :]
 
 
-def lane_noise(gen: LaneStream, S: int, N: int, sigma: float, with_bound: bool = False):
+def lane_noise(gen: LaneStream, S: int, N: int, sigma: float, with_bound: bool = False, radius_fn=None,
+               product_rel: float = 2.0 ** -24):
     """Complex noise (S, N) at the kept time samples, from outputs m2 .. m(E+1) of every lane
     (with_bound: and the (S, N) bound of noise_from_words)."""
     E, _ = geometry(N)
-    parts = [noise_from_words(gen.next(), sigma, with_bound) for _ in range(E)]
+    parts = [noise_from_words(gen.next(), sigma, with_bound, radius_fn, product_rel) for _ in range(E)]
     if not with_bound:
         return _lane_to_row(np.stack(parts, axis=1), S, N)
     return (_lane_to_row(np.stack([p[0] for p in parts], axis=1), S, N),
@@ -189,7 +204,8 @@ class PhiloxLink:
 
 def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq: str, snr_db: float,
                noise_on: bool = True, modulator: str = "OFDM", prefix: str = "CP",
-               scheme: str = "QAM", orders=None, precision: Optional[str] = None) -> PhiloxLink:
+               scheme: str = "QAM", orders=None, precision: Optional[str] = None, radius_fn=None,
+               power_sum: Optional[float] = None) -> PhiloxLink:
     """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic.
 
     modulator "OFDM" | "SC" (modulation/models.py:58-91), prefix "CP" | "ZP"
@@ -204,10 +220,16 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
 
     precision "f32" | "f64": also return the decision bracket of a GPU run in that arithmetic
     (PhiloxLink.bracket, see decision_bracket).
+
+    radius_fn: the GPU's noise radii of a word array (noise_from_words); power_sum: the GPU run's
+    whole-stream sum |y|^2 (its exact fixed-point value), from which sigma is computed as the
+    receivers compute it -- together they make the receivers' noise the restatement's bit for bit
+    in complex128 (the decision bracket then only covers FFT / FIR / equaliser rounding).
     """
     E, tps = geometry(N)
     gen = lane_generators(seed, np.arange(S), N)
     want_bound = precision is not None and noise_on
+    prel = 2.0 ** -53 if precision == "f64" else 2.0 ** -24
     if orders is not None:
         orders = np.asarray(orders, np.int64)
         bk = np.array([int(np.log2(o)) if o > 0 else 0 for o in orders], np.int64)
@@ -238,14 +260,17 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
         yk, tail = y[:, cp:].copy(), None
     rxs = yk.copy()
     nerr = np.zeros(S)  # per symbol: sum over its received samples of the noise deviation bound
+    nerr2 = np.zeros(S)  # ... and the sum of its squares
     if noise_on:
-        p = py / (S * (N + cp))
-        sigma = np.sqrt((p / 10 ** (snr_db / 10)) / 2.0)
+        # sigma^2 = mean |y|^2 / snr (noise/models.py:13-18), as k_rx evaluates it in double
+        p = (py if power_sum is None else float(power_sum)) / (S * (N + cp))
+        sigma = float(np.sqrt((p / 10 ** (snr_db / 10)) / 2.0))
         if want_bound:
-            nz, nb = lane_noise(gen, S, N, sigma, with_bound=True)
+            nz, nb = lane_noise(gen, S, N, sigma, with_bound=True, radius_fn=radius_fn, product_rel=prel)
             nerr += nb.sum(axis=1)
+            nerr2 += (nb ** 2).sum(axis=1)
         else:
-            nz = lane_noise(gen, S, N, sigma)
+            nz = lane_noise(gen, S, N, sigma, radius_fn=radius_fn)
         rxs = rxs + nz
     if prefix == "ZP" and cp > 0:
         if noise_on:
@@ -253,11 +278,12 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
             for i in range(E):
                 k = t + i * tps
                 w = gen.next()
-                n, nb = noise_from_words(w, sigma, with_bound=True)
+                n, nb = noise_from_words(w, sigma, with_bound=True, radius_fn=radius_fn, product_rel=prel)
                 use = k < cp
                 srow = np.repeat(np.arange(S), tps)[use]
                 tail[srow, k[use]] += n[use]
                 np.add.at(nerr, srow, nb[use])
+                np.add.at(nerr2, srow, nb[use] ** 2)
         rxs[:, :cp] += tail
     H = np.fft.fft(np.asarray(h_raw, np.complex128), N)
     Y = np.fft.fft(rxs, axis=1, norm="ortho")
@@ -266,7 +292,7 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
         Z = np.fft.ifft(Z, axis=1, norm="ortho")
     bracket = None
     if precision is not None:
-        delta = z_error_bound(precision, Y, H, eq, snr_db, nerr, modulator, N)
+        delta = z_error_bound(precision, Y, H, eq, snr_db, nerr, modulator, N, np.sqrt(nerr2))
         if orders is not None:
             bracket = adaptive_bracket(Z, idx, orders, bk, delta, scheme)
         else:
@@ -312,7 +338,7 @@ def adaptive_counts(diff: np.ndarray, bk: np.ndarray, S: int):
 # is empty of slack (lo = hi) unless a received point lies within the bound of a decision boundary.
 
 def z_error_bound(precision: str, Y: np.ndarray, H: np.ndarray, eq: str, snr_db: float,
-                  noise_err: np.ndarray, modulator: str, N: int) -> np.ndarray:
+                  noise_err: np.ndarray, modulator: str, N: int, noise_err2=None) -> np.ndarray:
     """(S, N) bound on the deviation of the GPU's equalised points from this restatement's.
 
     * noise: each received sample deviates by at most its noise_from_words bound; through the
@@ -323,8 +349,10 @@ def z_error_bound(precision: str, Y: np.ndarray, H: np.ndarray, eq: str, snr_db:
     * equaliser: the deviation times the subcarrier's gain |dZ/dY| (ZF 1/|H|, MMSE
       |H| / (|H|^2 + nv)), plus a relative term for the MMSE noise variance computed from the
       GPU's own received power;
-    * single carrier: the IFFT after the equaliser preserves the 2-norm, so the bound is the
-      2-norm of the per-subcarrier bounds."""
+    * single carrier: the IFFT after the equaliser preserves the 2-norm, so a sample deviates by at
+      most the 2-norm of the equalised deviation: max gain x (2-norm of the noise deviations,
+      noise_err2, + the arithmetic term) + the relative terms x ||Z||, plus the IFFT's own rounding
+      (c log2(N) u ||Z||)."""
     S = Y.shape[0]
     logn = max(1.0, np.log2(N))
     u = 2.0 ** -24 if precision == "f32" else 2.0 ** -53
@@ -346,7 +374,11 @@ def z_error_bound(precision: str, Y: np.ndarray, H: np.ndarray, eq: str, snr_db:
     Zabs = np.abs(Y) * g
     d = g * dy[:, None] + rel * Zabs + 1e-300
     if modulator == "SC":
-        d = np.broadcast_to(np.sqrt(np.sum(d ** 2, axis=1))[:, None], (S, N))
+        n2 = noise_err if noise_err2 is None else noise_err2
+        e2 = n2 + 6.0 * logn * u * np.sqrt(N) * rms  # 2-norm of the symbol's deviation (FFT: ortho)
+        z2 = np.sqrt(np.sum(Zabs ** 2, axis=1))
+        d = g.max(axis=1) * e2 + (rel + 6.0 * logn * u) * z2 + 1e-300
+        d = np.broadcast_to(d[:, None], (S, N))
     return np.asarray(d)
 
 

@@ -33,3 +33,21 @@ def test_float32_limbs_equal_double_limbs():
     # the value the limbs carry is p rounded to 2^-40
     v = h64.astype(np.float64) * 2.0 ** -8 + l64.astype(np.float64) * 2.0 ** -40
     assert np.all(np.abs(v - p.astype(np.float64)) <= 2.0 ** -41 * (1 + 1e-12) + np.abs(p) * 2.0 ** -52)
+
+
+def normalize(l0: np.ndarray, l1: np.ndarray):
+    """fx_normalize: carry limb 0's bits above 2^32 into limb 1."""
+    return l0 & np.uint64(0xFFFFFFFF), l1 + (l0 >> np.uint64(32))
+
+
+def test_double_share_whose_fraction_rounds_to_2_32_carries():
+    """A complex128 share whose fraction lies within 2^-41 of 1 rounds to exactly 2^32 units of
+    2^-40: fx_accum converts it through 64 bits (a 32-bit conversion of 2^32 is undefined and
+    the hardware clamps it to 2^32 - 1) and fx_normalize carries it into limb 1."""
+    p = np.array([(4096.0 + 1.0 - 2.0 ** -40) / 256.0, (1.0 - 2.0 ** -45) / 256.0, 2.0 ** 23 - 2.0 ** -33])
+    hi, lo = limbs_f64(p)
+    assert lo[0] == 2 ** 32 and lo[1] == 2 ** 32
+    l0, l1 = normalize(lo, hi)
+    v = l1.astype(np.float64) * 2.0 ** -8 + l0.astype(np.float64) * 2.0 ** -40
+    assert np.all(np.abs(v - p) <= 2.0 ** -41)
+    assert l1[0] == 4097 and l0[0] == 0

@@ -1,6 +1,7 @@
 """Size-independent properties of the throughput path at the benchmark's full sizes
-(BASELINE configs (b) and (e): 1e6 OFDM symbols of N = 1024, 2.5e5 of N = 4096 -- 8.2 GB of
-channel samples per launch), where the oracle cannot follow:
+(BASELINE configs (b) and (e): 1e6 OFDM symbols of N = 1024, 2.5e5 of N = 4096 -- 16.4 GB of
+channel samples per launch in complex128, the bench's headline precision, 8.2 GB in complex64),
+where the oracle cannot follow:
 
 * a noise-free link decodes every bit (map -> IFFT -> channel -> FFT -> equaliser -> slicer
   are exact inverses up to float rounding far below the decision distance);
@@ -27,23 +28,28 @@ FULL = [  # N, M, channel, equaliser, symbols, SNR dB
 ]
 
 
-def _engine(N, M, ch, eq):
+PRECS = pytest.mark.parametrize("prec", [B.OFDM_F64, B.OFDM_F32], ids=["c128", "c64"])
+
+
+def _engine(N, M, ch, eq, prec):
     h = channel(ch)
-    return LinkEngine(N, len(h) - 1, h, eq, [O.qam_lut(M)], None, B.OFDM_F32)
+    return LinkEngine(N, len(h) - 1, h, eq, [O.qam_lut(M)], None, prec)
 
 
+@PRECS
 @pytest.mark.parametrize("N,M,ch,eq,S,snr", FULL, ids=["b", "e"])
-def test_full_size_noise_free_is_error_free(gpu, N, M, ch, eq, S, snr):
-    eng = _engine(N, M, ch, eq)
+def test_full_size_noise_free_is_error_free(gpu, N, M, ch, eq, S, snr, prec):
+    eng = _engine(N, M, ch, eq, prec)
     r = eng.run(S, snr, seed=3, noise_on=False)
     assert r.bit_errors == 0 and r.symbol_errors == 0
     assert 0.9 < r.power_sum / r.samples < 1.1  # unit-power constellation, unit-power channel
     assert 8.0 < r.papr_db < 14.0
 
 
+@PRECS
 @pytest.mark.parametrize("N,M,ch,eq,S,snr", FULL, ids=["b", "e"])
-def test_full_size_counts_are_additive(gpu, N, M, ch, eq, S, snr):
-    eng = _engine(N, M, ch, eq)
+def test_full_size_counts_are_additive(gpu, N, M, ch, eq, S, snr, prec):
+    eng = _engine(N, M, ch, eq, prec)
     st = eng.stream()
     y = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
     stats = new_stats("cuda")
@@ -59,13 +65,15 @@ def test_full_size_counts_are_additive(gpu, N, M, ch, eq, S, snr):
     w, p = whole.cpu().numpy(), parts.cpu().numpy()
     assert w[0] > 1000 and np.array_equal(w, p), (w, p)
     # and the same run through the engine's own schedule
+    del y
     r = eng.run(S, snr, seed=7)
     assert (r.bit_errors, r.symbol_errors) == (int(w[0]), int(w[1]))
 
 
-def test_full_size_batching_invariance(gpu):
+@PRECS
+def test_full_size_batching_invariance(gpu, prec):
     N, M, ch, eq, S, snr = FULL[0]
-    eng = _engine(N, M, ch, eq)
+    eng = _engine(N, M, ch, eq, prec)
     a = eng.run(S, snr, seed=21)
     b = eng.run(S, snr, seed=21, batch=250_000)
     assert a.bit_errors > 1000

@@ -117,3 +117,33 @@ def test_noise_is_complex_gaussian():
 def test_oracle_link_noise_free_is_error_free():
     r = P.run_philox(2, 32, 1024, 64, np.array([0.8, 0.3j, 0.1]), 2, "MMSE", 30.0, noise_on=False)
     assert r.bit_errors == 0 and r.symbol_errors == 0
+
+
+def test_noise_table_entries_are_robust():
+    """The phase table's float32 cos / sin are the same whether a double cos is evaluated as the
+    kernels do (cospi((2j + 1) / 64)) or as the oracle does (cos(pi (2j + 1) / 64)): every exact
+    value lies far (> 1e-12 relative) from a float32 rounding midpoint, so any double evaluation
+    within a few ulp rounds to the same float32 -- the premise of restating the receivers' noise
+    bit for bit from their radii (philox_streams.noise_from_words(radius_fn=...))."""
+    th = np.pi * (2.0 * np.arange(P.NOISE_PHASES, dtype=np.longdouble) + 1.0) / P.NOISE_PHASES
+    for v in (np.cos(th), np.sin(th)):
+        f = v.astype(np.float32)
+        for g in (np.nextafter(f, np.float32(np.inf)), np.nextafter(f, np.float32(-np.inf))):
+            mid = (f.astype(np.longdouble) + g.astype(np.longdouble)) / 2
+            assert np.all(np.abs(v - mid) > 1e-12 * np.abs(v))
+    # the oracle's table entries are those float32 values times float32(sigma sqrt(2 ln 2))
+    t = P.noise_table(0.37)
+    sc = np.float32(0.37 * P.SQRT_2LN2)
+    assert np.array_equal(t.real, (sc * np.cos(th.astype(np.float64)).astype(np.float32)).astype(np.float64))
+
+
+def test_noise_from_given_radii():
+    """With the GPU's radii supplied, the noise is radius x table entry (exact in float64) and its
+    bound is the product rounding alone; the float64 radius stays within its own bound of it."""
+    w = np.random.default_rng(3).integers(0, 2 ** 32, size=20000, dtype=np.uint64).astype(np.uint32)
+    sig = 0.21
+    n64, b64 = P.noise_from_words(w, sig, with_bound=True)
+    rad = lambda ws: np.sqrt(32.0 - np.log2((ws | P.NOISE_MASK).astype(np.float32).astype(np.float64))).astype(np.float32)
+    n32, b32 = P.noise_from_words(w, sig, with_bound=True, radius_fn=rad, product_rel=2.0 ** -53)
+    assert np.all(np.abs(n32 - n64) <= b64)
+    assert np.all(b32 <= 2.0 ** -52 * np.abs(n32) + 1e-300)
