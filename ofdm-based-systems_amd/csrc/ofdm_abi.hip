@@ -717,11 +717,15 @@ static void fill_common(ofdm_plan_t p, TxRxCommon& c, const uint8_t* bits, uint6
     c.ystride = c.zpad ? p->n + p->cp : p->n;
     c.lut64 = (const double*)p->lut64.p;
     c.upat = p->upat;
-    // sector decisions for the reference's M-PSK in throughput mode (complex64, device bits) only:
-    // complex128 and the reference-stream mode keep the reference's nearest-point search
-    c.psk_m = (p->prec == OFDM_F32 && bits == nullptr) ? p->psk_m : 0;
-    for (int q = 0; q < 4; ++q)
-        c.psk_tan[q] = (c.psk_m >= 8 && q < c.psk_m / 8) ? (float)std::tan((q + 0.5) * 2.0 * M_PI / c.psk_m) : 0.f;
+    // sector decisions for the reference's M-PSK in throughput mode (device bits) on the throughput
+    // kernels; the reference-stream mode and the generic kernel keep the reference's nearest-point
+    // search (complex128: the same decisions except on a sector boundary, ~1e-16 relative)
+    c.psk_m = bits == nullptr ? p->psk_m : 0;
+    for (int q = 0; q < 4; ++q) {
+        const double tq = (c.psk_m >= 8 && q < c.psk_m / 8) ? std::tan((q + 0.5) * 2.0 * M_PI / c.psk_m) : 0.0;
+        c.psk_tan[q] = (float)tq;
+        c.psk_tan64[q] = tq;
+    }
 }
 
 int ofdm_tx(ofdm_plan_t p, void* stream, const uint8_t* bits, uint64_t seed, int64_t sym0, int64_t n_sym,

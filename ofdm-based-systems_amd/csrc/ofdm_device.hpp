@@ -1154,6 +1154,14 @@ struct Mwc64x {
         const f32x2 e = sample(next(), ntab, r);
         return f32x2{r, r} * e;
     }
+    // complex128 without the widened table (the generic kernel, zero-padding tail samples): the
+    // same exact product of the float32 radius and entry, fused into the sample
+    __device__ __forceinline__ void add_noise_f64(double& re, double& im, const f32x2* ntab) {
+        float r;
+        const f32x2 e = sample(next(), ntab, r);
+        re = __builtin_fma((double)r, (double)e.x, re);
+        im = __builtin_fma((double)r, (double)e.y, im);
+    }
     // complex128 kernels: the same radius and phase entry, the product taken in double against
     // ntab64 = the float32 table entries widened (exact), fused into the sample: one conversion
     // and two v_fma_f64 instead of a float product and two conversions.  Bits 3..8 of w address

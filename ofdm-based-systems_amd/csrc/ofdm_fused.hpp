@@ -203,17 +203,29 @@ constexpr bool tx_sep_lut() { return OFDM_TX_SEP_LUT && sizeof(R) == 8 && FB >= 
 #define OFDM_TX_BIG_WFIR_WAVES 3
 #endif
 // LDS of the complex128 FIR TX at blk threads (upper estimate of its Carve sequence, smem_tx):
-// FIR rows of fir_pad(N + 32) + 1 reals (window FIR: or the N / 2 transposed outputs, if more;
-// the run-time-tap FIR: complex) and the 7
-// complex tail samples per symbol, per-pass
-// twiddles, the static LUT (adaptive: the 512-entry pool and the per-subcarrier table), taps
+// FIR rows -- window FIR: half a symbol's stream as complex samples, wfir_slot(N/2 + 48) + 1 of
+// them (cp <= 32), or the FFT's N + N/16 reals if more; the run-time-tap FIR: fir_pad(N + 32) + 1
+// complex -- and the 7 complex tail samples per symbol, per-pass twiddles, the static LUT
+// (adaptive: the 512-entry pool and the per-subcarrier table), taps
 constexpr int f64_fir_lds(int fb, int logn, int blk, bool real_rows) {
     const int n = 1 << logn, tps = logn < 4 ? 1 : n >> 4, spb = blk / tps;
-    const int fir = (n + 32) + ((n + 32) >> 4) + 1, transpose = 2 * (n / 2 + n / 16);
-    const int rows = spb * ((real_rows ? (fir > transpose ? fir : transpose) * 8 : fir * 16) + 7 * 16);
+    const int fir = (n + 32) + ((n + 32) >> 4) + 1, half = 2 * (n / 2 + 48 + ((n / 2 + 48) >> 3) + 1);
+    const int padn = n + (n >> 4);
+    const int rows = spb * ((real_rows ? (half > padn ? half : padn) * 8 : fir * 16) + 7 * 16);
     const int tt = tt_size(logn) * 16;
     const int lut = fb == 1 ? (kMaxLut + 1) * 16 + 4 * n : (16 << fb);
     return rows + tt + lut + 1024;
+}
+// static (__shared__) LDS of the fused kernels beside their dynamic rows (kLdsPerCu checks)
+template <typename R, int FB>
+constexpr size_t rx_static_lds() {
+    return 8 * kNoisePhases + (sizeof(R) == 8 && FB > 0 ? 16 * kNoisePhases : 16);
+}
+template <typename R, int FB, int LT>
+constexpr size_t tx_static_lds() {
+    const size_t lut = FB == 1 ? kMaxLut + 1 : (FB > 1 ? ((size_t)1 << FB) : 1);
+    const size_t sep = (sizeof(R) == 8 && FB >= 2 && !(FB & 1) && LT != 0) ? 2 * ((size_t)1 << (FB / 2)) : 1;
+    return lut * 2 * sizeof(R) + sep * sizeof(R);
 }
 // LT (throughput TX): 0 flat channel; 4 / 8 multipath with <= LT taps through the register
 // window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps)
@@ -251,8 +263,8 @@ __host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
 // the OFDM_F64_RX_BLOCK / _WAVES shape: no-equaliser RX of 64/256-QAM at N = 1024 (at 128 VGPRs the
 // QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves;
 // with an equaliser the 16 KB coefficient table beside 16 symbols' rows exceeds the LDS)
-template <int FB, int LOGN, int EQ>
-constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10; }
+template <int FB, int LOGN, int EQ, bool MV = false>
+constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10 && !MV; }
 // (OFDM_F64_RX_SOLO_D: the same for the adaptive RX at N = 2048 (config d) -- 128-thread workgroups
 // of one symbol at 2 waves per SIMD, instead of four symbols per 512-thread workgroup: RX 5.12 ->
 // 4.67 ms, step 10.11 -> 9.93 ms per 5e5 symbols, profiles/r03ad_ab.txt)
@@ -264,19 +276,22 @@ constexpr bool f64_rx_solo() {
     return OFDM_F64_RX_SOLO && sizeof(R) == 8 &&
            ((FB > 1 && LOGN == 12) || (OFDM_F64_RX_SOLO_D && FB == 1 && LOGN == 11));
 }
-template <typename R, int FB, int LOGN, int EQ>
+// MV: the complex128 SC-OFDM / zero-padding kernels (k_rx MV), ~10-50 VGPRs above their cyclic-prefix
+// OFDM twins: never the 4-wave shape, and the one-symbol N = 4096 shape at 2 waves per SIMD
+template <typename R, int FB, int LOGN, int EQ, bool MV = false>
 constexpr int rx_block() {
     // (the adaptive kernel's per-order tables take ~200 VGPRs in complex128: 2 waves per SIMD)
     if (f64_rx_solo<R, FB, LOGN>()) return (1 << LOGN) / 16;  // one symbol
     if (sizeof(R) == 8 && FB > 0)
-        return (LOGN > 10 || FB == 1) ? 512 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_BLOCK : 768);
+        return (LOGN > 10 || FB == 1) ? 512 : (f64_rx_wide<FB, LOGN, EQ, MV>() ? OFDM_F64_RX_BLOCK : 768);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_BLOCK(LOGN);
     return FB > 1 && LOGN <= 10 && EQ == OFDM_EQ_NONE ? OFDM_RX_FAST_BLOCK : kBlock;
 }
-template <typename R, int FB, int LOGN, int EQ>
+template <typename R, int FB, int LOGN, int EQ, bool MV = false>
 constexpr int rx_waves() {
-    if (f64_rx_solo<R, FB, LOGN>()) return FB == 1 ? 2 : OFDM_F64_RX_SOLO_WAVES;
-    if (sizeof(R) == 8 && FB > 0) return (LOGN > 10 || FB == 1) ? 2 : (f64_rx_wide<FB, LOGN, EQ>() ? OFDM_F64_RX_WAVES : 3);
+    if (f64_rx_solo<R, FB, LOGN>()) return (FB == 1 || MV) ? 2 : OFDM_F64_RX_SOLO_WAVES;
+    if (sizeof(R) == 8 && FB > 0)
+        return (LOGN > 10 || FB == 1) ? 2 : (f64_rx_wide<FB, LOGN, EQ, MV>() ? OFDM_F64_RX_WAVES : 3);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;
     return rx_block<R, FB, LOGN, EQ>() >= 512 ? 4 : OFDM_RX_WAVES;
 }
@@ -415,7 +430,7 @@ __device__ __forceinline__ uint32_t psk_decide(cpx<R> v, const TxRxCommon& cm) {
         k = sx ? 1 : 0;
     } else {
         int q = 0;
-        for (int j = 0; j < (M >> 3); ++j) q += w > (R)cm.psk_tan[j] * u;
+        for (int j = 0; j < (M >> 3); ++j) q += w > (sizeof(R) == 8 ? (R)cm.psk_tan64[j] : (R)cm.psk_tan[j]) * u;
         const int quarter = M >> 2;
         int k1 = sw ? quarter - q : q;        // reflect about 45 degrees
         if (M == 4) k1 = sw ? 1 : 0;
@@ -485,14 +500,11 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     const bool adaptive = FB ? false : (bool)cm.adaptive;
     // generic kernel variants: single-carrier OFDM (no IFFT, modulation/models.py:
     // 58-70) and the zero-padding guard (prefix/models.py:55-67: [x | 0 ... 0])
-    // (the complex128 throughput kernels take OFDM with a cyclic prefix only: the launcher sends
-    // SC-OFDM and zero padding to the generic kernel, so both are compiled out of them)
-    constexpr bool F64_FAST = sizeof(R) == 8 && FB > 0;
-    const bool scm = (FB == 1 || F64_FAST) ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
+    const bool scm = FB == 1 ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
     // zero-padding guard (run-time, uniform); compiled out of the flat throughput TX (a zero
     // guard needs cp > 0, the launcher sends it to the LT = -1 kernel), where the run-time
     // row stride alone cost 15 % (config b TX 1.64 -> 1.92 ms)
-    constexpr bool ZP_OK = !(FB == 1 || (FB > 1 && LT == 0) || F64_FAST);
+    constexpr bool ZP_OK = !(FB == 1 || (FB > 1 && LT == 0));
     const bool zp = ZP_OK ? (bool)cm.zpad : false;
     const int ystride = ZP_OK ? cm.ystride : N;  // stored samples per OFDM symbol: N, or N + cp (ZP)
     const int cp = cm.cp, L = LT != 0 ? a.L : 1;
@@ -605,9 +617,10 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     const uint32_t v = (lane_word(tb.lane, I >> 2) >> (8 * (I & 3))) & e & 0xFFu;
                     x[I] = lut[(e >> 8) + v];
                 });
-            } else if constexpr (SEP) {
+            } else if (SEP && cm.psk_m == 0) {
                 // two 8-byte reads from SIDE-entry tables: distinct entries sit on distinct banks
-                // (the 2^FB-entry complex table's random 16-byte reads conflicted)
+                // (the 2^FB-entry complex table's random 16-byte reads conflicted); the reference's
+                // 4/16-PSK (not separable) take the complex table below
                 static_for<0, E>([&](auto I) {
                     const uint32_t v = tb.template fixed<I>();
                     x[I] = mk<R>(sep_s[v & (SIDE - 1)], sep_s[SIDE + (v >> HB)]);
@@ -701,19 +714,30 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                 static_assert(E == 16 && TPS >= 16, "window FIR geometry");
                 constexpr int WN = E + LT - 1;
                 if constexpr (sizeof(R) == 8) {
-                    // complex128: the row is a row of reals (half the LDS of a complex row: two
-                    // symbols per CU more at N >= 2048), so the stream goes through it twice, real
-                    // parts then imaginary parts, into the same register window.  Each output in
-                    // Gauss's three-multiplication form with the products accumulated as sums:
+                    // complex128: the FIR runs over the symbol in two halves of N / 2 kept samples,
+                    // through the symbol's row of reals used as complex samples, one pad slot per 8
+                    // (wfir_slot).  Half h holds the stream samples m in [cp + h N/2 - (LT-1),
+                    // cp + (h+1) N/2) at wfir_slot(B_h + m) -- half 0 from m = -(LT-1): the previous
+                    // symbol's tail and the prefix region too -- and lane t computes the 8
+                    // consecutive kept samples k = h N/2 + 8 t + j from a window of 8 + LT - 1
+                    // complex samples (ds_read_b128 at lane stride 9: conflict free), streamed one
+                    // sample at a time through the outputs' accumulators in Gauss's three-
+                    // multiplication form:
                     //   T = sum hr (wr + wi),  U = sum (hr + hi) wi,  V = sum (hi - hr) wr,
                     //   y = (T - U, T + V)
-                    // -- 3 v_fma_f64 per tap plus 2 adds per output and 1 per window sample,
-                    // instead of the 4 of a complex FMA.  The taps' three forms come with the
-                    // kernel arguments (TxArgs::gtap, zero past L) and stay in scalar registers:
-                    // the window and the accumulators fill the vector registers at LT = 8
+                    // (3 v_fma_f64 per tap and output; the taps' three forms in scalar registers,
+                    // TxArgs::gtap, zero past L).  Live at once: half a symbol's elements, 24
+                    // accumulators and the streamed sample -- against two whole windows of reals and
+                    // 16 outputs' sums when the row carried the real and then the imaginary parts.
+                    // The outputs leave through the row (kk = 8 t + j at wfir_slot(kk), read back as
+                    // kk = t + TPS i): lanes 8 m .. 8 m + 7 store one whole 128-byte line.
                     static_assert(LT <= kWinTaps, "window FIR taps");
-                    R* rr = (R*)row;
+                    constexpr int WH = 8 + LT - 1;
+                    C* crow = (C*)row;
+                    auto st16 = [&](int slot_, C v) { *(f64x2*)(crow + slot_) = f64x2{v.re, v.im}; };
+                    auto ld16 = [&](const C* p) { const f64x2 u = *(const f64x2*)p; return mk<R>(u.x, u.y); };
                     const bool live = active && c >= 0;
+                    const bool store = live && yout && !(flags & 4);
                     R hr[LT], c1[LT], c2[LT];
 #pragma unroll
                     for (int q = 0; q < LT; ++q) {
@@ -721,102 +745,103 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         c1[q] = a.gtap[1][q];
                         c2[q] = a.gtap[2][q];
                     }
-                    R wre[WN], wim[WN];
-                    R pT = 0, pU = 0, pV = 0;  // prefix-region output of lane t < cp
-#pragma unroll
-                    for (int P = 0; P < 2; ++P) {  // P = 0: real parts, 1: imaginary parts
-                        const bool IM = P == 1;
-                        sym_sync<TPS>();  // the FFT's last pass / the real parts' reads are done
-                        {
-                            const int bx = fir_pad(R0 + cp + t);  // stream sample cp + t + TPS i
-#pragma unroll
-                            for (int i = 0; i < E; ++i) rr[bx + TPS * i + (TPS * i >> 4)] = IM ? x[i].im : x[i].re;
-                        }
-                        if (t >= TPS - cp) rr[fir_pad(R0 + t - (TPS - cp))] = IM ? x[E - 1].im : x[E - 1].re;  // cyclic prefix
-                        if (t < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
-                            const int z = t - (LT - L);
-                            rr[fir_pad(R0 - (LT - 1) + t)] = z < 0 ? (R)0 : (IM ? tl[z].im : tl[z].re);
+                    // LDS offsets and lane conditions from opaque per-symbol copies of t, cp and L,
+                    // each offset a per-symbol base plus compile-time constants: hoisted out of the
+                    // symbol loop they were ~20 loop-invariant registers, spilled to scratch
+                    int to = t, cpo = cp, lo = L;
+                    asm volatile("" : "+v"(to), "+s"(cpo), "+s"(lo));
+                    const int A8 = (cpo + 7) & ~7;
+                    R pys = 0;
+                    static_for<0, 2>([&](auto HH) {
+                        constexpr int h = HH;
+                        constexpr int NH = N / 2;
+                        // stream sample m at wfir_slot(B + m); the lanes' windows start at Ah + 8 t
+                        const int Ah = h == 0 ? A8 : 0;
+                        const int B = Ah - cpo - h * NH + (LT - 1);
+                        sym_sync<TPS>();  // the FFT's last pass / the previous half's stores have read the row
+                        // this half's elements: kept k = t + TPS i (stream cp + k) for k in
+                        // [h N/2 - (LT-1), (h+1) N/2); TPS i = N/2 at i = 8
+                        // (TPS i = 0 mod 8: wfir_slot(b + TPS i) = wfir_slot(b) + 9 TPS i / 8)
+                        const int bx = wfir_slot(B + cpo + to);
+                        static_for<0, E>([&](auto I) {
+                            constexpr int i = I;
+                            constexpr int off = 9 * TPS * i / 8;
+                            if constexpr (i >= 8 * h && i < 8 * h + 8) {
+                                st16(bx + off, x[i]);
+                            } else if constexpr (h == 1 && i == 7) {
+                                if (to >= TPS - (LT - 1)) st16(bx + off, x[i]);
+                            }
+                        });
+                        if constexpr (h == 0) {
+                            if (to >= TPS - cpo) st16(wfir_slot(B + to - (TPS - cpo)), x[E - 1]);  // cyclic prefix
+                            if (to < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
+                                const int z = to - (LT - lo);
+                                st16(wfir_slot(B - (LT - 1) + to), z < 0 ? mk<R>(0, 0) : tl[z]);
+                            }
                         }
                         sym_sync<TPS>();
-                        {
-                            // every lane reads its window, live or not: read under the same
-                            // condition as the outputs, the two windows spilled (87-131 VGPRs)
-                            const R* wb = rr + (A + (A >> 4) + 17 * t);
-#pragma unroll
-                            for (int w = 0; w < WN; ++w) {
-                                if (IM) wim[w] = wb[w + (w >> 4)];
-                                else wre[w] = wb[w + (w >> 4)];
-                            }
-                            if (t < cp) {  // prefix-region outputs: power only (noise/models.py:14)
+                        if constexpr (h == 0) {
+                            // this symbol's tail for the next one, from the registers (the old tail
+                            // has been copied): its last L - 1 stream samples, lanes TPS - (L-1) ..
+                            if (to >= TPS - (lo - 1)) tl[to - (TPS - (lo - 1))] = active ? x[E - 1] : mk<R>(0, 0);
+                        }
+                        // every lane streams its window, live or not (under the live condition the
+                        // accumulators would be conditionally defined and spill)
+                        const C* wb = crow + (wfir_slot(Ah) + 9 * to);
+                        R T[8], U[8], V[8];
+                        static_for<0, WH>([&](auto W) {
+                            const C e = ld16(wb + (W + (W >> 3)));
+                            const R sw = e.re + e.im;
+                            static_for<0, LT>([&](auto Q) {  // tap Q of output j
+                                constexpr int j = W - (LT - 1) + Q;
+                                if constexpr (j >= 0 && j < 8) {
+                                    if constexpr (Q == LT - 1) {  // the output's first term
+                                        T[j] = hr[Q] * sw;
+                                        U[j] = c1[Q] * e.im;
+                                        V[j] = c2[Q] * e.re;
+                                    } else {
+                                        T[j] = __builtin_fma(hr[Q], sw, T[j]);
+                                        U[j] = __builtin_fma(c1[Q], e.im, U[j]);
+                                        V[j] = __builtin_fma(c2[Q], e.re, V[j]);
+                                    }
+                                }
+                            });
+                        });
+                        if constexpr (h == 0) {
+                            if (live && to < cpo) {  // prefix-region output m = t: power only (noise/models.py:14)
+                                R pT = 0, pU = 0, pV = 0;
 #pragma unroll
                                 for (int l = 0; l < LT; ++l) {
-                                    const R e = rr[fir_pad(R0 + t - l)];
-                                    pT = __builtin_fma(hr[l], e, pT);
-                                    if (IM) pU = __builtin_fma(c1[l], e, pU);
-                                    else pV = __builtin_fma(c2[l], e, pV);
+                                    const C e = ld16(crow + wfir_slot(B + to - l));
+                                    pT = __builtin_fma(hr[l], e.re + e.im, pT);
+                                    pU = __builtin_fma(c1[l], e.im, pU);
+                                    pV = __builtin_fma(c2[l], e.re, pV);
                                 }
+                                const R pr = pT - pU, pi = pT + pV;
+                                pys = __builtin_fma(pr, pr, pys);
+                                pys = __builtin_fma(pi, pi, pys);
                             }
                         }
-                        // this symbol's tail for the next one (every lane has copied the old one)
-                        if (t < L - 1) {
-                            const R v = active ? rr[fir_pad(R0 + N + cp - (L - 1) + t)] : (R)0;
-                            if (IM) tl[t].im = v;
-                            else tl[t].re = v;
-                        }
-                    }
-                    // The lane's outputs are the 16 consecutive samples k = 16 t + j: stored
-                    // directly, every store instruction would touch 64 cache lines (the
-                    // stores cost config e 1.7 ms of 5.7, profiles/r03t_ablate_e.txt).  They
-                    // go through the row instead, in two halves (j < 8, j >= 8), each N / 2
-                    // complex samples at wfir_slot(kk), kk = 8 t + j % 8, and leave as
-                    // kk = t + TPS i: lanes 8 m .. 8 m + 7 store one whole 128-byte line.
-                    C* crow = (C*)rr;
-                    C* ys = yout + sl * N;
-                    const bool store = live && yout && !(flags & 4);
-                    R pys = 0;
+                        sym_sync<TPS>();  // every window is read: the outputs take the row
 #pragma unroll
-                    for (int hh = 0; hh < 2; ++hh) {
-                        sym_sync<TPS>();  // the windows / the previous half's samples are read
-                        // (every lane computes, live or not, as it read its window: under the
-                        // live condition the windows spilled)
-#pragma unroll
-                        for (int jj = 0; jj < 8; ++jj) {
-                            const int j = 8 * hh + jj;
-                            R T = 0, U = 0, V = 0;
-#pragma unroll
-                            for (int l = 0; l < LT; ++l) {
-                                const int w = j + LT - 1 - l;
-                                T = __builtin_fma(hr[l], wre[w] + wim[w], T);
-                                U = __builtin_fma(c1[l], wim[w], U);
-                                V = __builtin_fma(c2[l], wre[w], V);
-                            }
-                            const C yv = mk<R>(T - U, T + V);
+                        for (int j = 0; j < 8; ++j) {
+                            const C yv = mk<R>(T[j] - U[j], T[j] + V[j]);
                             pys = __builtin_fma(yv.re, yv.re, pys);
                             pys = __builtin_fma(yv.im, yv.im, pys);
-                            crow[wfir_slot(8 * t + jj)] = yv;
+                            st16(9 * to + j, yv);  // wfir_slot(8 t + j)
                         }
                         sym_sync<TPS>();
                         if (store) {
-                            // lane offsets from an opaque copy of t: hoisted out of the symbol
-                            // loop they would hold 16 registers through the FFT
-                            int to = t;
-                            asm volatile("" : "+v"(to));
-                            const int k0 = 16 * (to >> 3) + 8 * hh + (to & 7);
                             // (the symbol's base is wave-uniform when a wave holds one symbol)
-                            gptr<C> yg = TPS >= 64 ? uniform_ptr(ys) : (gptr<C>)ys;
+                            C* yh = yout + sl * N + h * NH;
+                            gptr<C> yg = TPS >= 64 ? uniform_ptr(yh) : (gptr<C>)yh;
+                            const C* rb = crow + wfir_slot(to);
 #pragma unroll
                             for (int i = 0; i < 8; ++i)
-                                st_stream<TX_NT>(lane_ptr(yg, (uint32_t)(k0 + 2 * TPS * i)), crow[wfir_slot(to + TPS * i)]);
+                                st_stream<TX_NT>(lane_ptr(yg, (uint32_t)(to + TPS * i)), ld16(rb + 9 * TPS * i / 8));
                         }
-                    }
-                    if (live) {
-                        if (t < cp) {
-                            const R pr = pT - pU, pi = pT + pV;
-                            pys = __builtin_fma(pr, pr, pys);
-                            pys = __builtin_fma(pi, pi, pys);
-                        }
-                        fx_accum((R)pys, pq0, pq1);
-                    }
+                    });
+                    if (live) fx_accum((R)pys, pq0, pq1);
                     sym_sync<TPS>();
                 } else {
                     sym_sync<TPS>();  // the last FFT pass has read the row
@@ -965,10 +990,12 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
 
 // ============================================================ fused RX
 // EQ: OFDM_EQ_* fixed at compile time (throughput kernel) or -1 = from the plan.
-template <typename R, int LOGN, int EQ, int FB>
-__global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOGN, EQ>())) void k_rx(
+// MV: SC-OFDM and zero padding compiled in (run-time flags); complex128 compiles them out of the
+// cyclic-prefix OFDM kernels (rx_eq)
+template <typename R, int LOGN, int EQ, int FB, bool MV>
+__global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB, LOGN, EQ, MV>())) void k_rx(
     RxArgs a) {
-    constexpr int BLK = rx_block<R, FB, LOGN, EQ>();
+    constexpr int BLK = rx_block<R, FB, LOGN, EQ, MV>();
     using G = Geo<LOGN, BLK>;
     using C = cpx<R>;
     constexpr int N = G::N, E = G::E, TPS = G::TPS;
@@ -979,11 +1006,11 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
     // generic kernel variants: single-carrier OFDM (FFT -> equalise -> IFFT,
     // modulation/models.py:72-91), zero-padding guard (overlap-add, prefix/models.py:69-101)
     // and non-separable constellations (PSK: brute-force nearest point, constellation/models.py:19-27)
-    constexpr bool F64_FAST = sizeof(R) == 8 && FB > 0;  // OFDM + cyclic prefix only (see k_tx)
-    const bool scm = (FB == 1 || F64_FAST) ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
-    const bool zp = (FB == 1 || F64_FAST) ? false : (bool)cm.zpad;  // zero-padding guard (run-time, uniform)
+    constexpr bool F64_FAST = sizeof(R) == 8 && FB > 0;  // complex128 throughput kernels
+    const bool scm = (FB == 1 || !MV) ? false : (bool)cm.scm;  // SC-OFDM (run-time, uniform)
+    const bool zp = (FB == 1 || !MV) ? false : (bool)cm.zpad;  // zero-padding guard (run-time, uniform)
     const bool nn = FB ? false : (bool)cm.nn;
-    const int ystride = (FB == 1 || F64_FAST) ? N : cm.ystride;
+    const int ystride = (FB == 1 || !MV) ? N : cm.ystride;
     // odd bits per subcarrier (FB = 3, 5): the reference's 8- / 32-PSK only
     constexpr bool FB_PSK_ONLY = FB > 1 && (FB & 1);
     // noise phase table: static LDS at a link-time constant address, so a lane word's bits 3..8
@@ -1184,8 +1211,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
                 } else if constexpr (F64_FAST) {
                     tb.g.add_noise64(x[i].re, x[i].im, ntab64);
                 } else {
-                    const f32x2 n = tb.g.noise(ntab);
-                    x[i] = x[i] + mk<R>((R)n.x, (R)n.y);
+                    tb.g.add_noise_f64(x[i].re, x[i].im, ntab);
                 }
             }
         }
@@ -1201,8 +1227,12 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
                         v.re += sigma * (R)a.nr[sg * (N + cp) + N + k];
                         v.im += sigma * (R)a.ni[sg * (N + cp) + N + k];
                     } else if (noise) {
-                        const f32x2 n = tb.g.noise(ntab);
-                        v = v + mk<R>((R)n.x, (R)n.y);
+                        if constexpr (sizeof(R) == 8) {
+                            tb.g.add_noise_f64(v.re, v.im, ntab);
+                        } else {
+                            const f32x2 n = tb.g.noise(ntab);
+                            v = v + mk<R>(n.x, n.y);
+                        }
                     }
                     x[i] = x[i] + v;
                 }
@@ -1252,6 +1282,11 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
         }
         if (scm) {
             // single carrier: equalise every subcarrier, back to time with ifft(ortho)
+            if constexpr (EQ_LATE) {
+                load_coef4(1);
+                load_coef4(2);
+                load_coef4(3);
+            }
 #pragma unroll
             for (int i = 0; i < E; ++i)
                 if (eq != OFDM_EQ_NONE)
@@ -1316,9 +1351,11 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ>()), (rx_waves<R, FB, LOG
                 // four elements per lane word: slice, look up, compare, count
                 static_for<0, E / 4>([&](auto Q) {
                     constexpr int q = Q;
-                    if constexpr (EQ_LATE && q + 1 < E / 4) load_coef4(q + 1);
+                    if constexpr (EQ_LATE && q + 1 < E / 4) {
+                        if (!scm) load_coef4(q + 1);  // (single carrier: loaded before its equaliser)
+                    }
                     C z[4];
-                    if constexpr (MMSE_BATCH) {
+                    if (MMSE_BATCH && !scm) {
                         // conj(H) v / (|H|^2 + nv) with the four reciprocals from one
                         C c[4];
                         R dn[4], inv[4];

@@ -20,8 +20,8 @@ namespace ofdm {
 #define OFDM_LOGN_CASES(X) \
     X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 #define OFDM_FB_CASES(X) X(2) X(3) X(4) X(5) X(6) X(8)
-// complex128 throughput kernels: square QAM (4..256)
-#define OFDM_FB64_CASES(X) X(2) X(4) X(6) X(8)
+// complex128 throughput kernels: square QAM (4..256) and the reference's 4..32-PSK
+#define OFDM_FB64_CASES(X) X(2) X(3) X(4) X(5) X(6) X(8)
 #endif
 
 template <typename F>
@@ -35,6 +35,10 @@ static hipError_t set_smem(F fn, size_t bytes) {
 }
 
 constexpr int kFastMinLogN = 6;  // throughput specialisations for N >= 64
+// LDS per CU on gfx950: a throughput-kernel instantiation whose LDS would exceed it (a shape the plan
+// allows but the specialised layout cannot hold) runs the generic kernel instead of failing at
+// launch (tests/test_gpu_edges.py::test_lds_limit_shapes_run)
+constexpr size_t kLdsPerCu = 160 * 1024;
 
 static inline int clamp_grid(int64_t want) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, kMaxGrid));
@@ -127,15 +131,24 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     constexpr int BLK = tx_block<R, FB, LOGN, LT>();
     TxArgs a = a0;
     if (FB > 0 && LT > 0) {
-        // window FIR row: stream samples [-(LT-1), N+cp) at fir_pad(R0 + m)
-        const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
-        a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
-        // complex128: the row of reals also carries N / 2 complex outputs (wfir_slot) per half
-        if (sizeof(R) == 8) a.slot = std::max(a.slot, 2 * (wfir_slot((1 << LOGN) / 2 - 1) + 1));
+        if constexpr (sizeof(R) == 8) {
+            // complex128: the row of reals carries half a symbol's stream as complex samples, half 0's
+            // m in [-(LT-1), cp + N/2) at wfir_slot(A8 - cp + LT - 1 + m), and N / 2 transposed outputs
+            const int A8 = (a.c.cp + 7) & ~7;
+            a.slot = std::max(a.slot, 2 * (wfir_slot(A8 + (1 << LOGN) / 2 + LT - 2) + 1));
+            a.slot = std::max(a.slot, 2 * (wfir_slot((1 << LOGN) / 2 - 1) + 1));
+        } else {
+            // window FIR row: stream samples [-(LT-1), N+cp) at fir_pad(R0 + m)
+            const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
+            a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
+        }
     }
     const size_t sm = smem_tx<R>(LOGN, BLK, FB > 0 ? 0 : a.c.lut_len, a.c.words_per_sym, a.L, a.slot,
                                  uses_tt<R, LOGN, FB>() ? tt_size(LOGN) : 0, FB > 0 && LT > 0,
                                  FB == 1 ? (size_t)4 << LOGN : 0, FB > 0, split_rows<R, FB>() && LT >= 0);
+    if constexpr (FB > 0) {
+        if (sm + tx_static_lds<R, FB, LT>() > kLdsPerCu) return tx_launch<R, LOGN, 0, -1>(a0, grid, s);
+    }
     auto fn = k_tx<R, LOGN, FB, LT>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
@@ -166,11 +179,12 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
-        // complex128 throughput kernels: square QAM (fixed or adaptive loading), device bits, OFDM
-        // with a cyclic prefix
+        // complex128 throughput kernels: device bits; square QAM with adaptive loading (OFDM, cyclic
+        // prefix); fixed square QAM or the reference's 4..32-PSK, OFDM or SC-OFDM, cyclic prefix or
+        // zero padding
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && !a.c.scm && !a.c.zpad && !a.c.nn)
             return tx_fast<R, LOGN, 1>(a, grid, s);
-        if (!a.c.adaptive && a.c.bits == nullptr && !a.c.nn && !a.c.scm && !a.c.zpad) {
+        if (!a.c.adaptive && a.c.bits == nullptr && (!a.c.nn || a.c.psk_m > 0) && (a.c.b % 2 == 0 || a.c.psk_m > 0)) {
 #define OFDM_TX_FB64(F) \
     case F:                \
         return tx_fast<R, LOGN, F>(a, grid, s);
@@ -212,15 +226,18 @@ hipError_t launch_tx(int logn, const TxArgs& a, int* grid, hipStream_t s) {
 #undef OFDM_TX_CASE
 }
 
-template <typename R, int LOGN, int EQ, int FB>
+template <typename R, int LOGN, int EQ, int FB, bool MV>
 static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
-    constexpr int BLK = rx_block<R, FB, LOGN, EQ>();
+    constexpr int BLK = rx_block<R, FB, LOGN, EQ, MV>();
     const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym,
                                  uses_tt<R, LOGN, FB>() ? tt_size(LOGN) * (FB > 1 && a.c.scm ? 2 : 1) : 0,
                                  (FB == 1 ? 8 * (sizeof(R) == 8 ? sizeof(OrderParams64) : sizeof(OrderParams)) : 0) +
                                      (eq_in_lds<R, FB, LOGN, EQ>() ? ((size_t)2 * sizeof(R)) << LOGN : 0),
                                  FB > 0, split_rows<R, FB>());
-    auto fn = k_rx<R, LOGN, EQ, FB>;
+    if constexpr (FB > 0) {
+        if (sm + rx_static_lds<R, FB>() > kLdsPerCu) return rx_launch<R, LOGN, -1, 0, true>(a, grid, s);
+    }
+    auto fn = k_rx<R, LOGN, EQ, FB, MV>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
@@ -228,11 +245,14 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <typename R, int LOGN, int FB>
+// MV: the run-time modem variants (SC-OFDM, zero padding) compiled in.  complex128 builds them as
+// separate kernels: compiled into the cyclic-prefix OFDM kernels of the bench, their second
+// transform and guard overlap-add spilled the config (b) receiver (~70 dwords at 128 VGPRs)
+template <typename R, int LOGN, int FB, bool MV = true>
 static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
-    if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, FB>(a, grid, s);
-    if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, FB>(a, grid, s);
-    return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB>(a, grid, s);
+    if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, FB, MV>(a, grid, s);
+    if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, FB, MV>(a, grid, s);
+    return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB, MV>(a, grid, s);
 }
 
 // Throughput configuration (complex64, fixed square QAM or the reference's 4/8/16/32-PSK (psk_m > 0),
@@ -244,11 +264,12 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
             !a.c.scm && !a.c.zpad && !a.c.nn)
             return rx_eq<R, LOGN, 1>(a, grid, s);
-        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr && !a.c.nn && !a.c.scm &&
-            !a.c.zpad) {
-#define OFDM_RX_FB64(F) \
-    case F:                \
-        return rx_eq<R, LOGN, F>(a, grid, s);
+        if (!a.c.adaptive && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
+            (!a.c.nn || a.c.psk_m > 0) && (a.c.b % 2 == 0 || a.c.psk_m > 0)) {
+#define OFDM_RX_FB64(F)                                                              \
+    case F:                                                                              \
+        return (a.c.scm || a.c.zpad) ? rx_eq<R, LOGN, F, true>(a, grid, s)               \
+                                     : rx_eq<R, LOGN, F, false>(a, grid, s);
             switch (a.c.b) {
                 OFDM_FB64_CASES(OFDM_RX_FB64)
                 default: break;
@@ -272,7 +293,7 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
 #undef OFDM_RX_FB
         }
     }
-    return rx_launch<R, LOGN, -1, 0>(a, grid, s);
+    return rx_launch<R, LOGN, -1, 0, true>(a, grid, s);
 }
 
 template <typename R>

@@ -131,7 +131,8 @@ struct TxRxCommon {
     const double* lut64;
     int upat;  // every LUT has the reference's square-QAM level patterns (kUPat): adaptive fast path
     int psk_m;          // > 0: the single LUT is the reference's M-PSK (M <= 32): sector decisions
-    float psk_tan[4];   // tan((q + 1/2) 2 pi / M), q < M / 8
+    float psk_tan[4];   // tan((q + 1/2) 2 pi / M), q < M / 8 (complex64)
+    double psk_tan64[4];  // the same in double (complex128)
 };
 
 struct TxArgs {

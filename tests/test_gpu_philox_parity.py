@@ -63,6 +63,18 @@ CASES = [
     (4096, 64, "flat_fading", "NONE", 64, 20.0, B.OFDM_F64, {}),
     (256, 16, "severe_multipath", "MMSE", 512, 16.0, B.OFDM_F64, {"cp": 2}),
     (512, 4, "default_multipath", "ZF", 512, 12.0, B.OFDM_F64, {"cp": 0}),
+    # SURVEY 8(f) variants on the complex128 throughput kernels (the bench precision): SC-OFDM
+    # (FFT -> EQ -> IFFT), zero padding (run-time-tap FIR, overlap-add RX), 4/8/16/32-PSK sector
+    # decisions (FB = 2 / 3 / 4 / 5), N = 4096 with one symbol per workgroup
+    (1024, 64, "severe_multipath", "MMSE", 256, 20.0, B.OFDM_F64, {"modulator": "SC"}),
+    (1024, 16, "severe_multipath", "MMSE", 256, 21.0, B.OFDM_F64, {"prefix": "ZP"}),
+    (1024, 16, "severe_multipath", "MMSE", 128, 16.0, B.OFDM_F64, {"scheme": "PSK"}),
+    (1024, 8, "Lin-Phoong_P2", "MMSE", 128, 22.0, B.OFDM_F64, {"scheme": "PSK", "modulator": "SC", "prefix": "ZP"}),
+    (256, 32, "severe_multipath", "MMSE", 256, 24.0, B.OFDM_F64, {"scheme": "PSK", "prefix": "ZP"}),
+    (128, 4, "severe_multipath", "ZF", 1024, 10.0, B.OFDM_F64, {"scheme": "PSK", "prefix": "ZP"}),
+    (4096, 64, "Lin-Phoong_P1", "MMSE", 64, 22.0, B.OFDM_F64, {"modulator": "SC"}),
+    (2048, 16, "Lin-Phoong_P1", "MMSE", 128, 19.0, B.OFDM_F64, {"prefix": "ZP", "modulator": "SC"}),
+    (256, 16, "flat_fading", "NONE", 1024, 12.0, B.OFDM_F64, {"modulator": "SC"}),
     # SURVEY 8(f) variants on the generic kernel
     (64, 4, "Lin-Phoong_P2", "ZF", 2048, 20.0, B.OFDM_F32, {"modulator": "SC"}),
     (1024, 16, "severe_multipath", "MMSE", 256, 21.0, B.OFDM_F32, {"prefix": "ZP"}),
