@@ -49,9 +49,15 @@ CONFIGS = {
           "config (d): N_FFT=2048, adaptive bit loading (water-filling, desired SER 1e-3), Lin-Phoong_P1.npy "
           "(4 taps, cp=3), MMSE, AWGN 20 dB"),
     # 38.75 dB: the BER 1e-4 crossing of this config (profiles/r02g_ber_curve_e.json: 38.67 dB)
+    # (deliberately above the reference's 10..30 dB sweep of config/simulation_settings_waterfilling
+    # .json, where 256-QAM never reaches BER 1e-4; the kernels' cost does not depend on the SNR)
     "e": (4096, 256, "Lin-Phoong_P1", 1.0, "MMSE", 38.75,
-          "config (e): N_FFT=4096, 256-QAM, Lin-Phoong_P1.npy (4 taps, cp=3), MMSE, AWGN 38.75 dB"),
+          "config (e): N_FFT=4096, 256-QAM, Lin-Phoong_P1.npy (4 taps, cp=3), MMSE, AWGN 38.75 dB (its BER 1e-4 "
+          "crossing, above the reference's 10..30 dB sweep)"),
 }
+# BASELINE configs[2] / SURVEY 8(d): config (c) as an SNR sweep, 0..30 dB in 1 dB steps plus 0.25 dB
+# steps over 26..29 dB around the BER 1e-4 crossing (~27.7 dB) -- 40 points
+SWEEP_GRID = sorted(set([float(x) for x in range(0, 31)] + [26 + 0.25 * i for i in range(13)]))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PRECISIONS = {"f64": ("c128 (f64)", 16), "f32": ("c64 (f32)", 8)}
 
@@ -233,7 +239,20 @@ def pmc_traffic(key: str, symbols_per_launch: int):
     rec = pm.get(key)
     if not rec:
         return None
+    from ofdm_based_systems import _backend as B
+
+    if rec.get("build_id") != B.build_id():  # profiled on other kernel sources: not this build's traffic
+        return None
     return {k: v * symbols_per_launch / rec["symbols_per_launch"] for k, v in rec["bytes_per_launch"].items()}
+
+
+def build_id_or_none():
+    try:
+        from ofdm_based_systems import _backend as B
+
+        return B.build_id()
+    except OSError:  # pragma: no cover
+        return None
 
 
 # ---------------------------------------------------------------------------- ranks
@@ -398,6 +417,70 @@ def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp:
     return engine, rec
 
 
+def crossing(snrs, bers, target=1e-4):
+    """SNR where a BER curve crosses `target` (log10 BER linear in dB between grid points)."""
+    pts = sorted((q, b) for q, b in zip(snrs, bers) if b > 0)
+    for (s0, b0), (s1, b1) in zip(pts[:-1], pts[1:]):
+        if b0 >= target > b1:
+            l0, l1, lt = math.log10(b0), math.log10(b1), math.log10(target)
+            return s0 + (s1 - s0) * (l0 - lt) / (l0 - l1)
+    return None
+
+
+def reference_sweep(engine64, N, cp, snrs, symbols):
+    """BER of the reference-stream path (the reference's PCG64 bits and legacy normals through the
+    complex128 kernels, bit-exact with the reference NumPy code) at each SNR; outside any timing."""
+    out = []
+    for i, q in enumerate(snrs):
+        bits = np.random.Generator(np.random.PCG64(500 + i)).bytes(math.ceil(symbols * engine64.bps / 8))
+        rs = np.random.RandomState(500 + i)
+        nr = rs.normal(size=symbols * (N + cp))
+        ni = rs.normal(size=symbols * (N + cp))
+        r = engine64.run(symbols, q, bits=np.frombuffer(bits, np.uint8), normals=(nr, ni))
+        out.append(r.bit_errors / engine64.valid_bits(symbols))
+    return out
+
+
+def measure_sweep(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory):
+    """The SNR sweep as the bench step: every step runs all SWEEP_GRID points, `per_gpu` OFDM
+    symbols per GPU each (one complete run per point, new seed per point and step), pipelined
+    through LinkEngine.run_pipelined and symbol-sharded across ranks; W untimed steps, K timed."""
+    N = cfg[0]
+    engine = factory(cfg, precision)
+    total = per_gpu * rt.world
+    engine.reserve(total, 2, group=rt.group)
+    grid = SWEEP_GRID
+    for i in range(args.warmup):
+        for p in engine.run_pipelined(total, grid, [50_000 + 100 * i + k for k in range(len(grid))], group=rt.group):
+            p.result()
+    events = None if rt.cpu else []
+    rt.sync()
+    rt.barrier()
+    rt.sync()
+    t0 = time.perf_counter()
+    snrs = grid * args.steps
+    seeds = [1000 * st + k for st in range(args.steps) for k in range(len(grid))]
+    pend = engine.run_pipelined(total, snrs, seeds, group=rt.group, events=events)
+    errs = [p.result().bit_errors for p in pend]
+    rt.sync()
+    rt.barrier()
+    rt.sync()
+    elapsed = rt.max_over_ranks(time.perf_counter() - t0)
+    per_point = [sum(errs[k::len(grid)]) for k in range(len(grid))]
+    nbits = engine.valid_bits(total) * args.steps
+    bers = [e / nbits for e in per_point]
+    w = PRECISIONS[precision][1]
+    rec = {
+        "value": total * len(grid) * args.steps / elapsed,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "dtype": PRECISIONS[precision][0],
+        "roofline": roofline(events, N, engine.bps, engine.cp, w, None),
+        "sweep": {"snr_db": grid, "ber": bers, "bits_per_point": nbits, "points": len(grid),
+                  "symbols_per_point_per_step": total},
+    }
+    return engine, rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -417,6 +500,11 @@ def main():
     ap.add_argument("--ramp-seconds", type=float, default=0.25,
                     help="clock-ramp warmup before the value_after_ramp measurement (0: skip it)")
     ap.add_argument("--engine-factory", default=None, help=argparse.SUPPRESS)  # tests: module:function
+    ap.add_argument("--sweep", action="store_true",
+                    help="one step = the SNR sweep of BASELINE configs[2] (0..30 dB by 1 dB + 26..29 dB by 0.25 dB), "
+                         "--symbols per GPU per point (default 1e5 x 1024/N)")
+    ap.add_argument("--ref-symbols", type=int, default=12000,
+                    help="--sweep: reference-stream OFDM symbols per point near the BER 1e-4 crossing (26..29 dB)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -432,6 +520,8 @@ def main():
 
     cfg = CONFIGS[args.config]
     N, M, ch, ratio, eq_name, snr, desc = cfg
+    if args.sweep:
+        return sweep_main(rt, args, cfg, factory)
     per_gpu = args.symbols if args.symbols else 1_000_000 // max(1, N // 1024)
     total = per_gpu * rt.world
     engine, head = measure(rt, args, cfg, args.precision, per_gpu, factory, ramp=True)
@@ -464,6 +554,7 @@ def main():
             "symbols_per_step": total, "parallelism": f"symbol-sharded x{rt.world}",
         },
         "roofline": head["roofline"],
+        "build_id": build_id_or_none(),
         "path_hbm_fraction": head["path_hbm_fraction"],
         "ber": head["ber"],
     }
@@ -478,6 +569,56 @@ def main():
                                                    symbols=max(2000, 16000 * 1024 // N))
     if rt.rank == 0 and rt.world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
+    if rt.rank == 0:
+        print(json.dumps(out), flush=True)
+    rt.finish()
+
+
+def sweep_main(rt: Runtime, args, cfg, factory):
+    """--sweep: the BASELINE configs[2] measurement -- symbols/s over the whole SNR sweep and the
+    BER 1e-4 crossing of the timed runs against the reference-stream path's."""
+    N, M, ch, ratio, eq_name, snr, desc = cfg
+    if M == 0:
+        raise SystemExit("--sweep needs a fixed-order config (b or c)")
+    per_gpu = args.symbols if args.symbols else 100_000 // max(1, N // 1024)
+    engine, head = measure_sweep(rt, args, cfg, args.precision, per_gpu, factory)
+    total = per_gpu * rt.world
+    devices = rt.gather(rt.dev if not rt.cpu else "cpu")
+    sw = head["sweep"]
+    out = {
+        "metric": "OFDM symbols/sec (1/2/4/8 GPU) at N_FFT=1024 64-QAM; BER ΔdB vs ref",
+        "value": head["value"], "unit": "OFDM symbols/s", "n_gpus": rt.world, "devices": devices,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": head["dtype"],
+        "data": "synthetic: Philox4x32-10 / MWC64X bits and Box-Muller AWGN generated on the GPU per (seed, symbol)",
+        "config": {
+            "workload": f"{desc.split(',')[0]} as the BASELINE configs[2] SNR sweep: {sw['points']} points "
+                        f"(0..30 dB by 1 dB, 26..29 dB by 0.25 dB) x {per_gpu} OFDM symbols per GPU per point; "
+                        f"one step = the whole sweep",
+            "n_fft": N, "qam_order": M, "bits_per_ofdm_symbol": engine.bps, "cp": engine.cp, "channel": ch,
+            "equalizer": eq_name, "snr_db": "sweep", "symbols_per_step": total * sw["points"],
+            "parallelism": f"symbol-sharded x{rt.world}",
+        },
+        "roofline": head["roofline"],
+        "build_id": build_id_or_none(),
+        "sweep": sw,
+    }
+    c_phx = crossing(sw["snr_db"], sw["ber"])
+    out["ber_1e-4_crossing_db"] = {"throughput": c_phx}
+    if rt.rank == 0 and not args.no_ber_check and not rt.cpu:
+        near = [q for q in sw["snr_db"] if 26.0 <= q <= 29.0]
+        eng64 = make_engine(cfg, "f64")
+        ref = reference_sweep(eng64, N, engine.cp, near, max(1000, args.ref_symbols * 1024 // N))
+        c_ref = crossing(near, ref)
+        out["ber_1e-4_crossing_db"]["reference_streams"] = c_ref
+        out["ber_1e-4_crossing_db"]["reference_symbols_per_point"] = max(1000, args.ref_symbols * 1024 // N)
+        out["ber_1e-4_crossing_db"]["reference_ber"] = dict(zip(near, ref))
+        out["delta_db_at_1e-4"] = None if c_phx is None or c_ref is None else c_phx - c_ref
+        out["bar_db"] = 0.05
+    if rt.rank == 0 and rt.world == 1 and not args.no_cpu_baseline:
+        cpu_cfg = (N, M, ch, ratio, eq_name, 27.75, desc)
+        out["cpu_baseline"] = cpu_baseline(cpu_cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
+        out["cpu_baseline"]["sample"] += " (at the sweep's 27.75 dB point: the CPU cost does not depend on the SNR)"
     if rt.rank == 0:
         print(json.dumps(out), flush=True)
     rt.finish()

@@ -656,22 +656,17 @@ struct Slicer {
 
 // Throughput-mode slicer (complex64, square QAM with b = FB <= 8 bits).  Both axes per
 // packed op: y = z * inv_step - lev0 * inv_step is the level coordinate (offset (side-1)/2,
-// a half-integer).  OFDM_SLICER_CLAMP (default): one v_pk_fma_f32 computes y / (side-1) of
-// both axes with the instruction's clamp bit, i.e. clamped to [0, 1] (every point beyond the
-// outer levels decides the outer level), and a second one v * (side-1) + 1.5*2^23 leaves
-// round(y) in the low mantissa bits (round-to-nearest-even; a tie is a decision boundary,
-// probability zero under noise) -- two packed ops per element.  Otherwise y + 1.5*2^23
-// is clamped to [0, side-1] on the raw bits by two v_med3_i32 (four ops per element).  The levels
+// a half-integer).  One v_pk_fma_f32 computes y / (side-1) of both axes with the instruction's
+// clamp bit, i.e. clamped to [0, 1] (every point beyond the outer levels decides the outer
+// level), and a second one v * (side-1) + 1.5*2^23 leaves round(y) in the low mantissa bits
+// (round-to-nearest-even; a tie is a decision boundary, probability zero under noise) -- two
+// packed ops per element, where clamping y + 1.5*2^23 on the raw bits took four.  The levels
 // of four elements are gathered into one selector word (byte j = element j) and looked up
 // with v_perm_b32 in byte tables: four rx indices per instruction, byte-aligned like the
 // lane's tx bits (lane_bits).
-#ifndef OFDM_SLICER_CLAMP
-#define OFDM_SLICER_CLAMP 1
-#endif
 template <int FB>
 struct PermSlicer {
     static constexpr int SIDE = 1 << (FB / 2), HB = FB / 2;
-    static constexpr int MAGIC = 0x4B400000;  // bit pattern of 1.5 * 2^23
     static constexpr uint32_t BYTE_MASK = 0x01010101u * ((1u << FB) - 1u);
     f32x2 mul, add, magic, smax;
     uint32_t ti[4], tq[4];  // byte k: ipat[k] / qpat[k] << HB (k < SIDE)
@@ -680,7 +675,7 @@ struct PermSlicer {
     // when the FFT output is left unnormalised)
     __device__ void load(const AxisInfo& a, float scale) {
         // clamp form: the level coordinate divided by side - 1 (QPSK: side - 1 = 1)
-        const double span = OFDM_SLICER_CLAMP ? (double)(SIDE - 1) : 1.0;
+        const double span = (double)(SIDE - 1);
         const float is = (float)(a.inv_step * (double)scale / span);
         const float off = (float)(-a.lev0 * a.inv_step / span);
         mul = f32x2{is, is};
@@ -692,10 +687,6 @@ struct PermSlicer {
             ti[k >> 2] |= (uint32_t)a.ipat[k] << (8 * (k & 3));
             tq[k >> 2] |= ((uint32_t)a.qpat[k] << HB) << (8 * (k & 3));
         }
-    }
-    __device__ __forceinline__ static uint32_t clampl(float f) {
-        const int u = __builtin_bit_cast(int, f);
-        return (uint32_t)min(max(u, MAGIC), MAGIC + SIDE - 1);  // level in the low byte
     }
     // byte j of the result = table[byte j of sel]
     __device__ __forceinline__ static uint32_t lookup(const uint32_t (&tb)[4], uint32_t sel) {
@@ -716,21 +707,15 @@ struct PermSlicer {
         uint32_t li[4], lq[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if constexpr (OFDM_SLICER_CLAMP) {
-                // both axes clamped to [0, 1] by the clamp bit of v_pk_fma_f32 (tools/clamp_probe.hip)
-                f32x2 v;
-                asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(v) : "v"(z[j].v), "v"(mul), "v"(add));
-                // the rounded levels taken as a 64-bit integer: read back as a float2 whose lanes
-                // are bit-cast, the compiler used lane 0 for both axes (as in adaptive_diff)
-                uint64_t fb;
-                asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(fb) : "v"(v), "v"(smax), "v"(magic));
-                li[j] = (uint32_t)fb;  // level in the low byte
-                lq[j] = (uint32_t)(fb >> 32);
-            } else {
-                const f32x2 f = __builtin_elementwise_fma(z[j].v, mul, add) + magic;
-                li[j] = clampl(f.x);
-                lq[j] = clampl(f.y);
-            }
+            // both axes clamped to [0, 1] by the clamp bit of v_pk_fma_f32 (tools/clamp_probe.hip)
+            f32x2 v;
+            asm("v_pk_fma_f32 %0, %1, %2, %3 clamp" : "=v"(v) : "v"(z[j].v), "v"(mul), "v"(add));
+            // the rounded levels taken as a 64-bit integer: read back as a float2 whose lanes
+            // are bit-cast, the compiler used lane 0 for both axes (as in adaptive_diff)
+            uint64_t fb;
+            asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(fb) : "v"(v), "v"(smax), "v"(magic));
+            li[j] = (uint32_t)fb;  // level in the low byte
+            lq[j] = (uint32_t)(fb >> 32);
         }
         const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
                                                   __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
@@ -826,9 +811,9 @@ __device__ __forceinline__ uint32_t upat_lookup(uint32_t sel) {
 }
 
 // Per-order slicer constants in LDS (one entry per LUT of the plan, entry 7 = unused
-// subcarrier): level coordinate y = z * mul + add, clamp bound MAGIC + side - 1, and
-// meta = tx bit mask (1 << b) - 1 | (1 << b/2) << 8.  OFDM_SLICER_CLAMP: mul and add are
-// divided by side - 1 and smax holds side - 1 as a float (0 for the unused entry).
+// subcarrier): level coordinate y = z * mul + add divided by side - 1 (clamped to [0, 1]), smax
+// = side - 1 as a float (0 for the unused entry), and meta = tx bit mask (1 << b) - 1 |
+// (1 << b/2) << 8.
 struct OrderParams {
     float mul, add;
     uint32_t smax, meta;
@@ -864,7 +849,6 @@ __device__ __forceinline__ uint32_t adaptive_combine(const uint32_t (&li)[4], co
 template <bool SMALL>
 __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], const OrderParams* const (&op)[4],
                                                   uint32_t txw) {
-    constexpr int MAGIC = 0x4B400000;  // bit pattern of 1.5 * 2^23: round(y) in the low mantissa
     const f32x2 magic2 = f32x2{12582912.0f, 12582912.0f};
     uint32_t li[4], lq[4], meta[4];
 #pragma unroll
@@ -875,29 +859,17 @@ __device__ __forceinline__ uint32_t adaptive_diff(const cpx<float> (&z)[4], cons
         // The result is taken as a 64-bit integer: read back as a float2 whose lanes are then
         // bit-cast, the compiler used lane 0 for both (reproduced in a 15-line kernel)
         const f32x2 ma = *(const f32x2*)&op[j]->mul;
-        if constexpr (OFDM_SLICER_CLAMP) {
-            // clamp form (PermSlicer): (mul, add) hold the coordinate / (side - 1), clamped to
-            // [0, 1] by the clamp bit; smax holds side - 1 as a float, splatted by op_sel_hi
-            f32x2 v;
-            asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_hi:[0,1,0] clamp"
-                : "=v"(v)
-                : "v"(z[j].v), "v"(ma));
-            const f32x2 sm = *(const f32x2*)&op[j]->smax;
-            uint64_t f;
-            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(f) : "v"(v), "v"(sm), "v"(magic2));
-            li[j] = (uint32_t)f;
-            lq[j] = (uint32_t)(f >> 32);
-        } else {
-            uint64_t f;
-            asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_hi:[0,1,0]"
-                : "=v"(f)
-                : "v"(z[j].v), "v"(ma));
-            const float fx = __builtin_bit_cast(float, (uint32_t)f) + 12582912.0f;
-            const float fy = __builtin_bit_cast(float, (uint32_t)(f >> 32)) + 12582912.0f;
-            const int smax = (int)op[j]->smax;
-            li[j] = (uint32_t)min(max(__builtin_bit_cast(int, fx), MAGIC), smax);
-            lq[j] = (uint32_t)min(max(__builtin_bit_cast(int, fy), MAGIC), smax);
-        }
+        // (mul, add) hold the coordinate / (side - 1), clamped to [0, 1] by the clamp bit (as
+        // PermSlicer); smax holds side - 1 as a float, splatted by op_sel_hi
+        f32x2 v;
+        asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1] neg_hi:[0,1,0] clamp"
+            : "=v"(v)
+            : "v"(z[j].v), "v"(ma));
+        const f32x2 sm = *(const f32x2*)&op[j]->smax;
+        uint64_t f;
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(f) : "v"(v), "v"(sm), "v"(magic2));
+        li[j] = (uint32_t)f;
+        lq[j] = (uint32_t)(f >> 32);
         // opaque to the v_perm byte-provider combine, which otherwise merges the Q gather
         // into the I gather (seen with run-time clamp bounds: the Q axis vanished)
         asm("" : "+v"(li[j]), "+v"(lq[j]));

@@ -139,18 +139,12 @@ __device__ __forceinline__ T buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 // complex128 multipath TX of square QAM (the plan sends only separable LUTs to the throughput
 // kernels): map through the two axis tables instead of the complex LUT (TX c 5.13 -> 5.12, e 5.26
 // -> 5.17 ms per step, profiles/r03aa_ab.txt)
-#ifndef OFDM_TX_SEP_LUT
-#define OFDM_TX_SEP_LUT 1
-#endif
 template <typename R, int FB, int LT>
-constexpr bool tx_sep_lut() { return OFDM_TX_SEP_LUT && sizeof(R) == 8 && FB >= 2 && !(FB & 1) && LT != 0; }
+constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && LT != 0; }
 
 // complex128 RX with a symbol per wave: the channel samples through buffer loads (one address
 // VGPR, the element offsets in SGPRs) instead of four 64-bit VGPR addresses (RX b 3.09 -> 3.06,
 // c 3.75 -> 3.70 ms per step at the same occupancy, profiles/r03ab_ab.txt)
-#ifndef OFDM_RX_BUF
-#define OFDM_RX_BUF 1
-#endif
 
 // MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
 #ifndef OFDM_TX_MP_BLOCK
@@ -162,7 +156,7 @@ constexpr bool tx_sep_lut() { return OFDM_TX_SEP_LUT && sizeof(R) == 8 && FB >= 
 // per SIMD: one 768-thread workgroup of 12 symbols per CU), flat TX 128 (4 waves: 1024 threads).
 // A 4-wave RX (1024 threads, 128 VGPRs, 7 spilled) measured config b 1.646 -> 1.648e8 symbols/s,
 // within the run-to-run spread (profiles/r03k_ab_rx1024.txt); with the channel samples
-// buffer-loaded (OFDM_RX_BUF: 6 dwords spilled at 128) it gains: RX 3.09 -> 2.98 ms, 1.669 ->
+// buffer-loaded (6 dwords spilled at 128) it gains: RX 3.09 -> 2.98 ms, 1.669 ->
 // 1.693e8 symbols/s (profiles/r03ab_ab.txt) -- the no-equaliser RX takes 1024 threads at 4 waves.
 // The window-FIR TX passes the extended stream through its row of reals twice (real, then
 // imaginary parts), in 256-thread workgroups at 2 waves per SIMD: two or more workgroups per
@@ -254,9 +248,6 @@ __host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
 // at 2 waves per SIMD, one barrier coupling both symbols' FFT exchanges.  Config e RX 5.02 ->
 // 4.21 ms per 2.5e5 symbols (2 waves per SIMD: 4.63); the step gains less (9.99 -> 9.64 ms): the
 // TX that follows runs 0.4 ms slower at the power cap (profiles/r03y_ab.txt)
-#ifndef OFDM_F64_RX_SOLO
-#define OFDM_F64_RX_SOLO 1
-#endif
 #ifndef OFDM_F64_RX_SOLO_WAVES
 #define OFDM_F64_RX_SOLO_WAVES 3
 #endif
@@ -265,16 +256,12 @@ __host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
 // with an equaliser the 16 KB coefficient table beside 16 symbols' rows exceeds the LDS)
 template <int FB, int LOGN, int EQ, bool MV = false>
 constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10 && !MV; }
-// (OFDM_F64_RX_SOLO_D: the same for the adaptive RX at N = 2048 (config d) -- 128-thread workgroups
+// (the same for the adaptive RX at N = 2048 (config d) -- 128-thread workgroups
 // of one symbol at 2 waves per SIMD, instead of four symbols per 512-thread workgroup: RX 5.12 ->
 // 4.67 ms, step 10.11 -> 9.93 ms per 5e5 symbols, profiles/r03ad_ab.txt)
-#ifndef OFDM_F64_RX_SOLO_D
-#define OFDM_F64_RX_SOLO_D 1
-#endif
 template <typename R, int FB, int LOGN>
 constexpr bool f64_rx_solo() {
-    return OFDM_F64_RX_SOLO && sizeof(R) == 8 &&
-           ((FB > 1 && LOGN == 12) || (OFDM_F64_RX_SOLO_D && FB == 1 && LOGN == 11));
+    return sizeof(R) == 8 && ((FB > 1 && LOGN == 12) || (FB == 1 && LOGN == 11));
 }
 // MV: the complex128 SC-OFDM / zero-padding kernels (k_rx MV), ~10-50 VGPRs above their cyclic-prefix
 // OFDM twins: never the 4-wave shape, and the one-symbol N = 4096 shape at 2 waves per SIMD
@@ -300,9 +287,6 @@ constexpr int rx_waves() {
 #ifndef OFDM_EQ_LDS_MAX_LOGN
 #define OFDM_EQ_LDS_MAX_LOGN 11
 #endif
-#ifndef OFDM_EQ_PRE
-#define OFDM_EQ_PRE 1
-#endif
 // complex128 at N = 4096: the table (64 KB) fits beside two symbols' split rows and the compact
 // twiddles, and preloading 16 complex128 coefficients would spill
 template <typename R, int FB, int LOGN, int EQ>
@@ -317,9 +301,6 @@ constexpr bool rx_eq_late() { return f64_rx_solo<R, FB, LOGN>() && EQ > OFDM_EQ_
 // Newton steps) and nine products (Montgomery's batch inversion; ~3 roundings more than one
 // reciprocal each, well inside the decision bracket's 8 u of equaliser arithmetic).  RX c 3.80 ->
 // 3.75, e 4.21 -> 4.16 ms per step (profiles/r03y_ab.txt)
-#ifndef OFDM_MMSE_BATCH
-#define OFDM_MMSE_BATCH 1
-#endif
 // complex128 throughput kernels exchange FFT data through rows of reals (fft_reg_split)
 template <typename R, int FB>
 constexpr bool split_rows() { return sizeof(R) == 8 && FB > 0; }
@@ -789,8 +770,15 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         // accumulators would be conditionally defined and spill)
                         const C* wb = crow + (wfir_slot(Ah) + 9 * to);
                         R T[8], U[8], V[8];
+                        // the window streamed two samples ahead of its use; the scheduling barrier
+                        // keeps the compiler from issuing all 8 + LT - 1 reads at once (a whole
+                        // window of live registers at the peak of the kernel)
+                        C ring[3];
+                        ring[0] = ld16(wb);
+                        ring[1] = ld16(wb + 1);
                         static_for<0, WH>([&](auto W) {
-                            const C e = ld16(wb + (W + (W >> 3)));
+                            if constexpr (W + 2 < WH) ring[(W + 2) % 3] = ld16(wb + ((W + 2) + ((W + 2) >> 3)));
+                            const C e = ring[W % 3];
                             const R sw = e.re + e.im;
                             static_for<0, LT>([&](auto Q) {  // tap Q of output j
                                 constexpr int j = W - (LT - 1) + Q;
@@ -806,6 +794,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                                     }
                                 }
                             });
+                            __builtin_amdgcn_sched_barrier(0);
                         });
                         if constexpr (h == 0) {
                             if (live && to < cpo) {  // prefix-region output m = t: power only (noise/models.py:14)
@@ -1045,9 +1034,9 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     // behind it instead of stalling each element of the equaliser
     constexpr bool EQ_LATE = rx_eq_late<R, FB, LOGN, EQ>();
     constexpr bool EQ_PRE =
-        OFDM_EQ_PRE && !EQ_LDS && !EQ_LATE && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
+        !EQ_LDS && !EQ_LATE && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
     constexpr bool EQ_REG = EQ_PRE || EQ_LATE;  // coefficients in registers (ecoef)
-    constexpr bool MMSE_BATCH = OFDM_MMSE_BATCH && sizeof(R) == 8 && FB > 1 && EQ == OFDM_EQ_MMSE;
+    constexpr bool MMSE_BATCH = sizeof(R) == 8 && FB > 1 && EQ == OFDM_EQ_MMSE;
 
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     const bool noise = a.noise_on && !(flags & 1);
@@ -1079,14 +1068,13 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     } else if constexpr (FB == 1) {
         if (threadIdx.x < 8) {
             // unused subcarrier: level 0, no bits
-            OrderParams o{0.f, 0.f, OFDM_SLICER_CLAMP ? 0u : 0x4B400000u, 0u};
+            OrderParams o{0.f, 0.f, 0u, 0u};
             if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
                 const AxisInfo ax = cm.axis[threadIdx.x];
-                const double span = OFDM_SLICER_CLAMP ? (double)(ax.side - 1) : 1.0;  // see OrderParams
+                const double span = (double)(ax.side - 1);  // see OrderParams
                 o.mul = (float)(ax.inv_step * cm.scale / span);  // the FFT output stays unscaled
                 o.add = (float)(-ax.lev0 * ax.inv_step / span);
-                o.smax = OFDM_SLICER_CLAMP ? __float_as_uint((float)(ax.side - 1))
-                                           : 0x4B400000u + (uint32_t)(ax.side - 1);
+                o.smax = __float_as_uint((float)(ax.side - 1));
                 o.meta = ((1u << ax.bits) - 1u) | ((1u << ax.hbits) << 8);
             }
             ordt[threadIdx.x] = o;
@@ -1155,7 +1143,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     // kept channel samples of local symbol sl.  Past the end the wave reads the last symbol
     // again (its results are neither counted nor stored): an unconditional load, where zeroing
     // the 16 elements cost 32 v_mov_b64 per symbol in complex128.  Zeros when ablated.
-    constexpr bool RX_BUF = OFDM_RX_BUF && F64_FAST && TPS == 64;
+    constexpr bool RX_BUF = F64_FAST && TPS == 64;
     auto load_sym = [&](int64_t sl, C (&dst)[E]) {
         const C* ys = (const C*)a.y + (sl < cm.n_sym ? sl : cm.n_sym - 1) * ystride;
         if (RX_BUF && !(flags & 16)) {

@@ -112,6 +112,24 @@ def lib_path() -> str:
     return _LIB_PATH
 
 
+def build_id() -> str:
+    """Identity of the kernel sources the library is built from: sha256 (16 hex digits) over the
+    HIP sources, the C-ABI header and the Makefile.  Profiles record it (profiles/pmc_summary.json)
+    so that bench.py reports PMC traffic only for the build it was measured on."""
+    import hashlib
+
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # ofdm-based-systems_amd/
+    root = os.path.dirname(pkg)
+    files = sorted(os.path.join(pkg, "csrc", f) for f in os.listdir(os.path.join(pkg, "csrc")))
+    files += [os.path.join(root, "include", "ofdm_hip.h"), os.path.join(pkg, "Makefile")]
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def load_library() -> ctypes.CDLL:
     """Load the library and bind every symbol of the header (no GPU needed)."""
     global _lib

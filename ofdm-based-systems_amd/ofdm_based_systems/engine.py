@@ -253,7 +253,7 @@ class LinkEngine:
         return PendingLink(n_sym, samples, stats, counters, z_out, done, work)
 
 
-    def run_pipelined(self, n_sym: int, snr_db: float, seeds, *, group=None,
+    def run_pipelined(self, n_sym: int, snr_db, seeds, *, group=None,
                       events: Optional[list] = None, y_budget: int = DEFAULT_Y_BUDGET) -> list:
         """Independent throughput-mode runs (one per seed) of global OFDM symbols [0, n_sym),
         software-pipelined across runs: run k+1's TX is enqueued before run k's RX, so with
@@ -261,7 +261,15 @@ class LinkEngine:
         TX -> RX path) is in flight while the GPU transmits run k+1.  Every run is complete
         and its counts are those of :meth:`run_async` with the same seed; returns the
         PendingLink of each run.  Two runs' channel samples are live at once; when they do not
-        fit ``y_budget`` the runs go through :meth:`run_async` one after another (batched)."""
+        fit ``y_budget`` the runs go through :meth:`run_async` one after another (batched).
+
+        snr_db: one SNR for every run, or one per seed -- an SNR sweep (the reference's one
+        Simulation per SNR point, simulation/models.py:190-211, run in order by main.py:234-239),
+        its points pipelined the same way (the SNR enters only the receiver)."""
+        seeds = list(seeds)
+        snrs = list(snr_db) if isinstance(snr_db, (list, tuple, np.ndarray)) else [snr_db] * len(seeds)
+        if len(snrs) != len(seeds):
+            raise ValueError("one SNR per seed")
         dev = self.device()
         stream = self.stream()
         world, rank = 1, 0
@@ -276,8 +284,8 @@ class LinkEngine:
         n_valid = self.valid_bits(n_sym)
         csize = 8 if self.cdtype == torch.complex64 else 16
         if 2 * max(mine, 1) * self.ystride * csize > y_budget:
-            return [self.run_async(n_sym, snr_db, seed=s, group=group, events=events, y_budget=y_budget)
-                    for s in seeds]
+            return [self.run_async(n_sym, q, seed=s, group=group, events=events, y_budget=y_budget)
+                    for s, q in zip(seeds, snrs)]
 
         def tx(seed):
             stats = new_stats(dev)
@@ -291,14 +299,14 @@ class LinkEngine:
                 work = (dist.all_gather(parts, stats, group=group, async_op=True), parts)
             return seed, y, stats, work
 
-        def rx(state):
+        def rx(state, snr):
             seed, y, stats, work = state
             if work is not None:  # reduce the gathered statistics (as run_async)
                 work[0].wait()
                 combine_stats(stats, work[1])
             counters = torch.zeros(2, dtype=torch.int64, device=dev)
             self._timed(events, "ofdm_rx", mine, lambda: self.rx(
-                stream, y, None, None, seed, stats, samples, snr_db, True, None, lo, mine, n_valid, counters))
+                stream, y, None, None, seed, stats, samples, snr, True, None, lo, mine, n_valid, counters))
             red = None
             if world > 1:
                 import torch.distributed as dist
@@ -309,12 +317,11 @@ class LinkEngine:
                 done.record()
             return PendingLink(n_sym, samples, stats, counters, None, done, red)
 
-        seeds = list(seeds)
         out = []
         cur = tx(seeds[0]) if seeds else None
         for k in range(len(seeds)):
             nxt = tx(seeds[k + 1]) if k + 1 < len(seeds) else None
-            out.append(rx(cur))
+            out.append(rx(cur, snrs[k]))
             cur = nxt
         return out
 

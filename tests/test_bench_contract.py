@@ -67,3 +67,35 @@ def test_bench_gpus_flag_launches_ranks():
     assert d["n_gpus"] == 2 and d["devices"] == ["cpu", "cpu"]
     assert d["config"]["symbols_per_step"] == 6 and d["scaling"] == "weak"
     assert d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+
+
+def test_sweep_grid_and_crossing():
+    """--sweep: BASELINE configs[2]'s 0..30 dB in 1 dB steps plus SURVEY 8(d)'s 0.25 dB refinement
+    over 26..29 dB; the crossing interpolates log10 BER linearly in dB."""
+    g = bench.SWEEP_GRID
+    assert len(g) == 40 and g[0] == 0.0 and g[-1] == 30.0 and 27.75 in g and 26.25 in g
+    assert abs(bench.crossing([20.0, 21.0], [1e-3, 1e-5]) - 20.5) < 1e-12
+    assert bench.crossing([20.0, 21.0], [1e-3, 1e-3]) is None
+
+
+def test_bench_sweep_two_ranks():
+    """`bench.py --sweep --gpus 2`: one step = every point of the sweep, sharded over the ranks,
+    pipelined through run_pipelined (one SNR per run); the line carries the per-point BER."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
+                                         os.path.join(ROOT, "ofdm-based-systems_amd"), env.get("PYTHONPATH", "")])
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--engine-factory", "bench_double:make_engine", "--config", "c", "--sweep", "--symbols", "1",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-ber-check"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["config"]["symbols_per_step"] == 80
+    sw = d["sweep"]
+    assert sw["points"] == 40 and len(sw["ber"]) == 40 and sw["snr_db"] == bench.SWEEP_GRID
+    assert sw["ber"][0] > sw["ber"][-1]  # 0 dB vs 30 dB

@@ -1,9 +1,9 @@
 """Throughput of the fused path per modem variant (SURVEY 8(a) configs and the 8(f) rows).
 
-Times ofdm_tx / ofdm_rx with HIP events on the launch stream, throughput mode (complex64,
-bits and noise generated in the kernels), one GPU:
+Times ofdm_tx / ofdm_rx with HIP events on the launch stream, throughput mode (bits and noise
+generated in the kernels), complex128 (the reference's arithmetic, default) or complex64, one GPU:
 
-    python tools/bench_variants.py [--symbols 1000000] [--steps 5] > gpurun_out/variants.json
+    python tools/bench_variants.py [--precision f64|f32] [--symbols 1000000] [--steps 5] > gpurun_out/variants.json
 
 Prints one JSON object per variant and a summary table on stderr.  Which kernel runs:
 square QAM or the reference's 4/16-PSK, OFDM or SC-OFDM, cyclic prefix or zero padding ->
@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--symbols", type=int, default=1_000_000)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--only", default="", help="comma-separated variant name prefixes (e.g. b,d)")
+    ap.add_argument("--precision", default="f64", choices=("f64", "f32"))
     args = ap.parse_args()
     only = [o for o in args.only.split(",") if o]
     torch.cuda.set_device(0)
@@ -81,7 +82,7 @@ def main():
             M = 2.0 ** (bps / N)  # mean bits per subcarrier, for the BER denominator
         else:
             luts = [(QAMConstellationMapper(M) if scheme == "QAM" else PSKConstellationMapper(M)).constellation]
-        eng = LinkEngine(N, cp, h, EQ[eq], luts, sc, B.OFDM_F32,
+        eng = LinkEngine(N, cp, h, EQ[eq], luts, sc, B.OFDM_F64 if args.precision == "f64" else B.OFDM_F32,
                          prefix=B.PREFIX_ZERO if pre == "ZP" else B.PREFIX_CYCLIC,
                          modulator=B.MOD_SC if mod == "SC" else B.MOD_OFDM)
         S = args.symbols if N <= 1024 else args.symbols // (N // 1024)
@@ -99,7 +100,7 @@ def main():
         ms = {}
         for kname, n, e0, e1 in ev:
             ms.setdefault(kname, []).append(e0.elapsed_time(e1))
-        row = {"variant": name, "n_fft": N, "order": M, "scheme": scheme, "modulator": mod, "prefix": pre,
+        row = {"variant": name, "precision": args.precision, "n_fft": N, "order": M, "scheme": scheme, "modulator": mod, "prefix": pre,
                "channel": ch, "equalizer": eq, "snr_db": snr, "symbols_per_step": S,
                "ofdm_symbols_per_s": S / dt,
                "ms_per_1e6_symbols": {k: float(np.mean(v)) * 1e6 / S for k, v in ms.items()},

@@ -33,7 +33,7 @@ def kernel_key(name: str):
     if ("<float" if PREC == "f32" else "<double") not in name or "<" not in name:
         return None
     args = [a.strip() for a in name[name.index("<") + 1:name.index(">")].split(",")]
-    if "k_rx" in name and len(args) == 4 and int(args[3]) > 0:
+    if "k_rx" in name and len(args) >= 4 and int(args[3]) > 0:  # k_rx<R, LOGN, EQ, FB, MV>
         return "ofdm_rx"
     if "k_tx" in name and len(args) == 4 and int(args[2]) > 0:
         return "ofdm_tx"
@@ -77,14 +77,18 @@ def main():
     summary = {"tag": tag, "config": config, "precision": PREC, "symbols_per_launch": syms, "kernels": durations,
                "hbm_per_launch": per_launch,
                "correction": "read_bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write_bytes = WRITE_SIZE x 1024"}
-    with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
-        json.dump(summary, f, indent=1)
     pm_path = os.path.join(prof, "pmc_summary.json")
     pm = json.load(open(pm_path)) if os.path.exists(pm_path) else {}
-    pm[key] = {"tag": tag, "symbols_per_launch": syms,
-                  "bytes_per_launch": {k: v["total_bytes"] for k, v in per_launch.items()}}
+    sys.path.insert(0, os.path.join(ROOT, "ofdm-based-systems_amd"))
+    from ofdm_based_systems._backend import build_id
+
+    pm[key] = {"tag": tag, "symbols_per_launch": syms, "build_id": build_id(),
+               "bytes_per_launch": {k: v["total_bytes"] for k, v in per_launch.items()}}
+    summary["build_id"] = pm[key]["build_id"]
     with open(pm_path, "w") as f:
         json.dump(pm, f, indent=1)
+    with open(os.path.join(prof, f"{tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))
 
 
