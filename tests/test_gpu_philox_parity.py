@@ -190,16 +190,18 @@ def bracket_width_bound(prec, var, count):
     receivers' noise bit for bit (their radii, their sigma), so only FFT / FIR / equaliser rounding
     at 2^-53 remains -- the counts are pinned to within 2 (in practice exactly, width 0).
     complex64: the float32 transforms' rounding, bounded through the 2-norm (philox_streams.
-    z_error_bound), leaves up to ~8 % of the count at N = 4096 / 256-QAM; single-carrier
-    complex64 spreads the worst subcarrier's equaliser gain over every sample and is not bounded
-    here (its width is printed)."""
+    z_error_bound), leaves up to ~8 % of the count at N = 4096 / 256-QAM and a few tens of counts on
+    the ~200-error adaptive cases (asserted <= max(64, 10 %)); single-carrier complex64 spreads the
+    worst subcarrier's equaliser gain over every sample and is not bounded here (its width is
+    printed)."""
     if prec == B.OFDM_F64:
         return max(2, count // 1000)
-    return None if var.get("modulator") == "SC" else max(8, count // 10)
+    return None if var.get("modulator") == "SC" else max(64, count // 10)
 
 
 @pytest.mark.parametrize("N,M,ch,eq,S,snr,prec,var", CASES, ids=IDS)
 def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
+    case_id = _id((N, M, ch, eq, S, snr, prec, var))
     eng, h, cp, var = setup(N, M, ch, eq, prec, var, snr)
     seed = 77
     res = eng.run(S, snr, seed=seed)
@@ -207,7 +209,7 @@ def test_error_counts_match_oracle(gpu, N, M, ch, eq, S, snr, prec, var):
                        radius_fn=gpu_radius, power_sum=res.power_sum, **var)
     assert ref.bit_errors > 100, "SNR too high for a meaningful count"
     be_lo, be_hi, se_lo, se_hi = ref.bracket
-    print(f"bracket {_id((N, M, ch, eq, S, snr, prec, var))}: bits {res.bit_errors} in [{be_lo}, {be_hi}] "
+    print(f"bracket {case_id}: bits {res.bit_errors} in [{be_lo}, {be_hi}] "
           f"(width {be_hi - be_lo}), symbols {res.symbol_errors} in [{se_lo}, {se_hi}] (width {se_hi - se_lo})")
     assert be_lo <= ref.bit_errors <= be_hi and se_lo <= ref.symbol_errors <= se_hi
     assert be_lo <= res.bit_errors <= be_hi, (res.bit_errors, ref.bracket)
