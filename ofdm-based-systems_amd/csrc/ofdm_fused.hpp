@@ -712,6 +712,11 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     // 16 outputs' sums when the row carried the real and then the imaginary parts.
                     // The outputs leave through the row (kk = 8 t + j at wfir_slot(kk), read back as
                     // kk = t + TPS i): lanes 8 m .. 8 m + 7 store one whole 128-byte line.
+                    // Zero padding (prefix/models.py:55-67, the stream [x | 0 ... 0]): x starts at
+                    // stream sample 0 instead of cp, every one of the N + cp outputs is stored
+                    // (ystride N + cp: the receiver overlap-adds the guard), the guard outputs
+                    // N + t (t < cp) from the last LT - 1 samples of x in half 1's row, and the
+                    // tail for the next symbol from that row too (the stream ends in the guard).
                     static_assert(LT <= kWinTaps, "window FIR taps");
                     constexpr int WH = 8 + LT - 1;
                     C* crow = (C*)row;
@@ -731,19 +736,20 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     // symbol loop they were ~20 loop-invariant registers, spilled to scratch
                     int to = t, cpo = cp, lo = L;
                     asm volatile("" : "+v"(to), "+s"(cpo), "+s"(lo));
-                    const int A8 = (cpo + 7) & ~7;
+                    const int so = zp ? 0 : cpo;  // stream sample of x[0]
+                    const int A8 = (so + 7) & ~7;
                     R pys = 0;
                     static_for<0, 2>([&](auto HH) {
                         constexpr int h = HH;
                         constexpr int NH = N / 2;
                         // stream sample m at wfir_slot(B + m); the lanes' windows start at Ah + 8 t
                         const int Ah = h == 0 ? A8 : 0;
-                        const int B = Ah - cpo - h * NH + (LT - 1);
+                        const int B = Ah - so - h * NH + (LT - 1);
                         sym_sync<TPS>();  // the FFT's last pass / the previous half's stores have read the row
                         // this half's elements: kept k = t + TPS i (stream cp + k) for k in
                         // [h N/2 - (LT-1), (h+1) N/2); TPS i = N/2 at i = 8
                         // (TPS i = 0 mod 8: wfir_slot(b + TPS i) = wfir_slot(b) + 9 TPS i / 8)
-                        const int bx = wfir_slot(B + cpo + to);
+                        const int bx = wfir_slot(B + so + to);
                         static_for<0, E>([&](auto I) {
                             constexpr int i = I;
                             constexpr int off = 9 * TPS * i / 8;
@@ -754,7 +760,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             }
                         });
                         if constexpr (h == 0) {
-                            if (to >= TPS - cpo) st16(wfir_slot(B + to - (TPS - cpo)), x[E - 1]);  // cyclic prefix
+                            if (!zp && to >= TPS - cpo) st16(wfir_slot(B + to - (TPS - cpo)), x[E - 1]);  // cyclic prefix
                             if (to < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
                                 const int z = to - (LT - lo);
                                 st16(wfir_slot(B - (LT - 1) + to), z < 0 ? mk<R>(0, 0) : tl[z]);
@@ -764,7 +770,14 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         if constexpr (h == 0) {
                             // this symbol's tail for the next one, from the registers (the old tail
                             // has been copied): its last L - 1 stream samples, lanes TPS - (L-1) ..
-                            if (to >= TPS - (lo - 1)) tl[to - (TPS - (lo - 1))] = active ? x[E - 1] : mk<R>(0, 0);
+                            if (!zp && to >= TPS - (lo - 1)) tl[to - (TPS - (lo - 1))] = active ? x[E - 1] : mk<R>(0, 0);
+                        } else {
+                            // zero padding: the last L - 1 stream samples N + cp - (L-1) + z are x
+                            // below N, guard zeros from N on
+                            if (zp && to < lo - 1) {
+                                const int m = N + cpo - (lo - 1) + to;
+                                tl[to] = (active && m < N) ? ld16(crow + wfir_slot(B + m)) : mk<R>(0, 0);
+                            }
                         }
                         // every lane streams its window, live or not (under the live condition the
                         // accumulators would be conditionally defined and spill)
@@ -796,8 +809,27 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             });
                             __builtin_amdgcn_sched_barrier(0);
                         });
+                        if constexpr (h == 1) {
+                            // zero padding: guard output N + t = sum over l > t of h_l x[N + t - l]
+                            // (the guard's own samples are zero), stored and counted
+                            if (zp && live && to < cpo) {
+                                R pT = 0, pU = 0, pV = 0;
+#pragma unroll
+                                for (int l = 1; l < LT; ++l) {
+                                    if (l <= to) continue;
+                                    const C e = ld16(crow + wfir_slot(B + N + to - l));
+                                    pT = __builtin_fma(hr[l], e.re + e.im, pT);
+                                    pU = __builtin_fma(c1[l], e.im, pU);
+                                    pV = __builtin_fma(c2[l], e.re, pV);
+                                }
+                                const C yv = mk<R>(pT - pU, pT + pV);
+                                pys = __builtin_fma(yv.re, yv.re, pys);
+                                pys = __builtin_fma(yv.im, yv.im, pys);
+                                if (store) yout[sl * ystride + N + to] = yv;
+                            }
+                        }
                         if constexpr (h == 0) {
-                            if (live && to < cpo) {  // prefix-region output m = t: power only (noise/models.py:14)
+                            if (!zp && live && to < cpo) {  // prefix-region output m = t: power only (noise/models.py:14)
                                 R pT = 0, pU = 0, pV = 0;
 #pragma unroll
                                 for (int l = 0; l < LT; ++l) {
@@ -822,7 +854,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         sym_sync<TPS>();
                         if (store) {
                             // (the symbol's base is wave-uniform when a wave holds one symbol)
-                            C* yh = yout + sl * N + h * NH;
+                            C* yh = yout + sl * ystride + h * NH;
                             gptr<C> yg = TPS >= 64 ? uniform_ptr(yh) : (gptr<C>)yh;
                             const C* rb = crow + wfir_slot(to);
 #pragma unroll

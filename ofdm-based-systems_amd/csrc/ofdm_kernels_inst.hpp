@@ -4,6 +4,9 @@
 #pragma once
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "ofdm_kernels.hpp"
 
@@ -126,6 +129,45 @@ hipError_t launch_awgn(const AwgnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Workgroups of a kernel resident on the device at once (occupancy x CUs), cached per kernel,
+// device, workgroup size and dynamic LDS; 0 when the runtime cannot say.
+template <typename F>
+static int resident_blocks(F fn, int blk, size_t smem) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void*, int, int, size_t>, int> cached;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    const auto key = std::make_tuple(reinterpret_cast<const void*>(fn), dev, blk, smem);
+    std::lock_guard<std::mutex> lock(mu);
+    const auto it = cached.find(key);
+    if (it != cached.end()) return it->second;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), blk, smem) !=
+            hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return cached[key] = 0;
+    }
+    return cached[key] = per_cu * cus;
+}
+
+// Symbols per multipath symbol group (each group regenerates its predecessor's tail once): the
+// chunk in [max / 2, max] whose rounds of resident workgroups times (chunk + 1) symbols per group
+// is least.  A launch of 1e5 symbols (one point of an SNR sweep) at chunk 32 needed 1.5 rounds of
+// workgroups -- two, the second half empty; chunk 25 fits it in two full rounds of 26-symbol
+// groups instead of 33.
+static inline int tx_chunk(int64_t n_sym, int max_chunk, int spb, int resident) {
+    if (resident <= 0 || n_sym <= 0) return max_chunk;
+    int best = max_chunk;
+    int64_t best_cost = -1;
+    for (int ch = max_chunk; ch >= (max_chunk + 1) / 2; --ch) {
+        const int64_t blocks = ((n_sym + ch - 1) / ch + spb - 1) / spb;
+        const int64_t cost = ((blocks + resident - 1) / resident) * (ch + 1);
+        if (best_cost < 0 || cost < best_cost) best_cost = cost, best = ch;
+    }
+    return best;
+}
+
 template <typename R, int LOGN, int FB, int LT>
 static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     constexpr int BLK = tx_block<R, FB, LOGN, LT>();
@@ -152,6 +194,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     auto fn = k_tx<R, LOGN, FB, LT>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
+    if (a.chunk > 1) a.chunk = tx_chunk(a.c.n_sym, a.chunk, Geo<LOGN, BLK>::SPB, resident_blocks(fn, BLK, sm));
     const int64_t groups = (a.c.n_sym + a.chunk - 1) / a.chunk;
     *grid = clamp_grid((groups + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
@@ -164,7 +207,8 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     constexpr int TPS = Geo<LOGN>::TPS;
     if (a.L == 1 && !a.c.zpad) return tx_launch<R, LOGN, FB, 0>(a, grid, s);
     if constexpr (LOGN >= 8) {
-        if (a.c.cp <= TPS && !a.c.zpad) {  // the register window assumes a cyclic prefix
+        // the complex64 register window assumes a cyclic prefix; the complex128 one takes zero padding
+        if (a.c.cp <= TPS && (!a.c.zpad || sizeof(R) == 8)) {
             if (a.L <= 4) return tx_launch<R, LOGN, FB, 4>(a, grid, s);
             if (a.L <= 8) return tx_launch<R, LOGN, FB, 8>(a, grid, s);
         }
