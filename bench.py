@@ -331,7 +331,7 @@ class Runtime:
             dist.destroy_process_group()
 
 
-def timed_steps(rt: Runtime, engine, total: int, snr: float, steps: int, seed0: int, events):
+def timed_steps(rt: Runtime, engine, total: int, snr: float, steps: int, seed0: int, events, lanes: int = 1):
     """K complete runs (one per step), enqueued as LinkEngine.run_pipelined schedules them and
     read back inside the timed region, bracketed by barrier + device synchronisation; the
     elapsed time is the maximum over ranks."""
@@ -339,7 +339,8 @@ def timed_steps(rt: Runtime, engine, total: int, snr: float, steps: int, seed0: 
     rt.barrier()
     rt.sync()
     t0 = time.perf_counter()
-    pending = engine.run_pipelined(total, snr, range(seed0, seed0 + steps), group=rt.group, events=events)
+    pending = engine.run_pipelined(total, snr, range(seed0, seed0 + steps), group=rt.group, events=events,
+                                   lanes=lanes)
     bit_errors = sum(p.result().bit_errors for p in pending)
     rt.sync()
     rt.barrier()
@@ -378,11 +379,11 @@ def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp:
     total = per_gpu * rt.world
     # the two runs' channel-sample buffers the pipelined schedule keeps alive, allocated before
     # the warmup (a first-time hipMalloc of 2 x 16.4 GB would otherwise land in the timed steps)
-    engine.reserve(total, 2, group=rt.group)
+    engine.reserve(total, 2, group=rt.group, lanes=args.lanes)
     for i in range(args.warmup):
         engine.run(total, snr, seed=10_000 + i, group=rt.group)
     events = None if rt.cpu else []
-    elapsed, bit_errors = timed_steps(rt, engine, total, snr, args.steps, 0, events)
+    elapsed, bit_errors = timed_steps(rt, engine, total, snr, args.steps, 0, events, args.lanes)
     w = PRECISIONS[precision][1]
     key = args.config if precision == "f32" else f"{args.config}_{precision}"
     rec = {
@@ -411,7 +412,7 @@ def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp:
                 break
             engine.run(total, snr, seed=20_000 + extra, group=rt.group)
             extra += 1
-        e2, _ = timed_steps(rt, engine, total, snr, args.steps, 30_000, None)
+        e2, _ = timed_steps(rt, engine, total, snr, args.steps, 30_000, None, args.lanes)
         rec["value_after_ramp"] = {"value": total * args.steps / e2, "ms_per_step": e2 / args.steps * 1e3,
                                    "extra_untimed_steps": extra, "ramp_seconds": args.ramp_seconds}
     return engine, rec
@@ -448,10 +449,11 @@ def measure_sweep(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory)
     N = cfg[0]
     engine = factory(cfg, precision)
     total = per_gpu * rt.world
-    engine.reserve(total, 2, group=rt.group)
+    engine.reserve(total, 2, group=rt.group, lanes=args.lanes)
     grid = SWEEP_GRID
     for i in range(args.warmup):
-        for p in engine.run_pipelined(total, grid, [50_000 + 100 * i + k for k in range(len(grid))], group=rt.group):
+        for p in engine.run_pipelined(total, grid, [50_000 + 100 * i + k for k in range(len(grid))], group=rt.group,
+                                      lanes=args.lanes):
             p.result()
     events = None if rt.cpu else []
     rt.sync()
@@ -460,7 +462,7 @@ def measure_sweep(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory)
     t0 = time.perf_counter()
     snrs = grid * args.steps
     seeds = [1000 * st + k for st in range(args.steps) for k in range(len(grid))]
-    pend = engine.run_pipelined(total, snrs, seeds, group=rt.group, events=events)
+    pend = engine.run_pipelined(total, snrs, seeds, group=rt.group, events=events, lanes=args.lanes)
     errs = [p.result().bit_errors for p in pend]
     rt.sync()
     rt.barrier()
@@ -503,6 +505,8 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="one step = the SNR sweep of BASELINE configs[2] (0..30 dB by 1 dB + 26..29 dB by 0.25 dB), "
                          "--symbols per GPU per point (default 1e5 x 1024/N)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="HIP streams the timed runs alternate over (LinkEngine.run_pipelined)")
     ap.add_argument("--ref-symbols", type=int, default=12000,
                     help="--sweep: reference-stream OFDM symbols per point near the BER 1e-4 crossing (26..29 dB)")
     args = ap.parse_args()

@@ -143,10 +143,17 @@ class LinkEngine:
                                   int(sym0), int(n_sym), int(n_valid), B.ptr(counters), B.ptr(z_out),
                                   int(z_keep)))
 
-    def reserve(self, n_sym: int, runs_in_flight: int = 2, group=None) -> None:
+    def reserve(self, n_sym: int, runs_in_flight: int = 2, group=None, lanes: int = 1) -> None:
         """Allocate, and hand back to torch's caching allocator, the channel-sample buffers of
         ``runs_in_flight`` concurrent runs of n_sym global symbols (run_pipelined keeps two
-        alive), so that later runs reuse them instead of paying for a multi-GB hipMalloc."""
+        alive), so that later runs reuse them instead of paying for a multi-GB hipMalloc; with
+        lanes > 1, the same on each of run_pipelined's lane streams (the allocator pools buffers
+        per stream)."""
+        if lanes > 1 and self.device().type == "cuda":
+            for st in self.lane_streams(lanes):
+                with torch.cuda.stream(st):
+                    self.reserve(n_sym, runs_in_flight, group)
+            return
         world, rank = 1, 0
         if group is not None:
             import torch.distributed as dist
@@ -253,8 +260,20 @@ class LinkEngine:
         return PendingLink(n_sym, samples, stats, counters, z_out, done, work)
 
 
+    def lane_streams(self, lanes: int) -> list:
+        """The current stream and lanes - 1 more, kept per engine (their allocator pools persist:
+        reserve() fills them before a timed region)."""
+        cur = torch.cuda.current_stream()
+        if lanes <= 1 or self.device().type != "cuda":
+            return [cur]
+        extra = getattr(self, "_lanes", [])
+        while len(extra) < lanes - 1:
+            extra.append(torch.cuda.Stream())
+        self._lanes = extra
+        return [cur] + extra[:lanes - 1]
+
     def run_pipelined(self, n_sym: int, snr_db, seeds, *, group=None,
-                      events: Optional[list] = None, y_budget: int = DEFAULT_Y_BUDGET) -> list:
+                      events: Optional[list] = None, y_budget: int = DEFAULT_Y_BUDGET, lanes: int = 1) -> list:
         """Independent throughput-mode runs (one per seed) of global OFDM symbols [0, n_sym),
         software-pipelined across runs: run k+1's TX is enqueued before run k's RX, so with
         several ranks the statistics exchange of run k (the one collective on a run's
@@ -265,7 +284,12 @@ class LinkEngine:
 
         snr_db: one SNR for every run, or one per seed -- an SNR sweep (the reference's one
         Simulation per SNR point, simulation/models.py:190-211, run in order by main.py:234-239),
-        its points pipelined the same way (the SNR enters only the receiver)."""
+        its points pipelined the same way (the SNR enters only the receiver).
+
+        lanes: HIP streams the runs alternate over (run k on lane k mod lanes, each run's TX,
+        exchanges and RX in order on its lane): with 2, one run's receiver overlaps the next run's
+        transmitter -- the launch tails and the one-workgroup statistics kernel between them of
+        short runs (a sweep's points) fill with the other lane's work.  One y buffer per lane."""
         seeds = list(seeds)
         snrs = list(snr_db) if isinstance(snr_db, (list, tuple, np.ndarray)) else [snr_db] * len(seeds)
         if len(snrs) != len(seeds):
@@ -287,19 +311,34 @@ class LinkEngine:
             return [self.run_async(n_sym, q, seed=s, group=group, events=events, y_budget=y_budget)
                     for s, q in zip(seeds, snrs)]
 
-        def tx(seed):
-            stats = new_stats(dev)
-            y = torch.empty((max(mine, 1), self.ystride), dtype=self.cdtype, device=dev)
-            self._timed(events, "ofdm_tx", mine, lambda: self.tx(stream, None, seed, lo, mine, y, stats))
-            work = None
-            if world > 1:
-                import torch.distributed as dist
+        lane_list = self.lane_streams(lanes) if lanes > 1 else None
 
-                parts = [torch.empty_like(stats) for _ in range(world)]
-                work = (dist.all_gather(parts, stats, group=group, async_op=True), parts)
+        def on(k):
+            """Context of run k's lane (the current stream when not alternating)."""
+            import contextlib
+
+            return torch.cuda.stream(lane_list[k % len(lane_list)]) if lane_list else contextlib.nullcontext()
+
+        def tx(k):
+            seed = seeds[k]
+            with on(k):
+                st = self.stream()
+                stats = new_stats(dev)
+                y = torch.empty((max(mine, 1), self.ystride), dtype=self.cdtype, device=dev)
+                self._timed(events, "ofdm_tx", mine, lambda: self.tx(st, None, seed, lo, mine, y, stats))
+                work = None
+                if world > 1:
+                    import torch.distributed as dist
+
+                    parts = [torch.empty_like(stats) for _ in range(world)]
+                    work = (dist.all_gather(parts, stats, group=group, async_op=True), parts)
             return seed, y, stats, work
 
-        def rx(state, snr):
+        def rx(state, snr, k):
+            with on(k):
+                return rx_on(state, snr, self.stream())
+
+        def rx_on(state, snr, stream):
             seed, y, stats, work = state
             if work is not None:  # reduce the gathered statistics (as run_async)
                 work[0].wait()
@@ -318,10 +357,10 @@ class LinkEngine:
             return PendingLink(n_sym, samples, stats, counters, None, done, red)
 
         out = []
-        cur = tx(seeds[0]) if seeds else None
+        cur = tx(0) if seeds else None
         for k in range(len(seeds)):
-            nxt = tx(seeds[k + 1]) if k + 1 < len(seeds) else None
-            out.append(rx(cur, snrs[k]))
+            nxt = tx(k + 1) if k + 1 < len(seeds) else None
+            out.append(rx(cur, snrs[k], k))
             cur = nxt
         return out
 
