@@ -176,6 +176,9 @@ constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && L
 #ifndef OFDM_F64_RX_WAVES
 #define OFDM_F64_RX_WAVES 4
 #endif
+#ifndef OFDM_F64_RX_WIDE_EQ
+#define OFDM_F64_RX_WIDE_EQ 0
+#endif
 #ifndef OFDM_F64_FIR_BLOCK
 #define OFDM_F64_FIR_BLOCK 256
 #endif
@@ -255,7 +258,15 @@ __host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
 // QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves;
 // with an equaliser the 16 KB coefficient table beside 16 symbols' rows exceeds the LDS)
 template <int FB, int LOGN, int EQ, bool MV = false>
-constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10 && !MV; }
+constexpr bool f64_rx_wide() {
+    return (EQ == OFDM_EQ_NONE || OFDM_F64_RX_WIDE_EQ) && FB >= 6 && LOGN == 10 && !MV;
+}
+// (OFDM_F64_RX_WIDE_EQ: A/B of the 4-wave shape with an equaliser -- the coefficients buffer-loaded
+// after the FFT (rx_eq_late) instead of a 16 KB LDS table, which does not fit beside 16 symbols)
+template <typename R, int FB, int LOGN, int EQ>
+constexpr bool f64_rx_wide_eq() {
+    return OFDM_F64_RX_WIDE_EQ && sizeof(R) == 8 && EQ > OFDM_EQ_NONE && FB >= 6 && LOGN == 10;
+}
 // (the same for the adaptive RX at N = 2048 (config d) -- 128-thread workgroups
 // of one symbol at 2 waves per SIMD, instead of four symbols per 512-thread workgroup: RX 5.12 ->
 // 4.67 ms, step 10.11 -> 9.93 ms per 5e5 symbols, profiles/r03ad_ab.txt)
@@ -292,11 +303,13 @@ constexpr int rx_waves() {
 template <typename R, int FB, int LOGN, int EQ>
 constexpr bool eq_in_lds() {
     return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= (sizeof(R) == 8 ? 12 : OFDM_EQ_LDS_MAX_LOGN) &&
-           !f64_rx_solo<R, FB, LOGN>();
+           !f64_rx_solo<R, FB, LOGN>() && !f64_rx_wide_eq<R, FB, LOGN, EQ>();
 }
 // the lane's coefficients loaded after the FFT (in flight across the MMSE power reduction)
 template <typename R, int FB, int LOGN, int EQ>
-constexpr bool rx_eq_late() { return f64_rx_solo<R, FB, LOGN>() && EQ > OFDM_EQ_NONE; }
+constexpr bool rx_eq_late() {
+    return (f64_rx_solo<R, FB, LOGN>() || f64_rx_wide_eq<R, FB, LOGN, EQ>()) && EQ > OFDM_EQ_NONE;
+}
 // MMSE in complex128: the reciprocals of |H|^2 + nv of four elements from one v_rcp_f64 (+ two
 // Newton steps) and nine products (Montgomery's batch inversion; ~3 roundings more than one
 // reciprocal each, well inside the decision bracket's 8 u of equaliser arithmetic).  RX c 3.80 ->
