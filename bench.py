@@ -379,11 +379,12 @@ def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp:
     total = per_gpu * rt.world
     # the two runs' channel-sample buffers the pipelined schedule keeps alive, allocated before
     # the warmup (a first-time hipMalloc of 2 x 16.4 GB would otherwise land in the timed steps)
-    engine.reserve(total, 2, group=rt.group, lanes=args.lanes)
+    lanes = args.lanes or 1
+    engine.reserve(total, 2, group=rt.group, lanes=lanes)
     for i in range(args.warmup):
         engine.run(total, snr, seed=10_000 + i, group=rt.group)
     events = None if rt.cpu else []
-    elapsed, bit_errors = timed_steps(rt, engine, total, snr, args.steps, 0, events, args.lanes)
+    elapsed, bit_errors = timed_steps(rt, engine, total, snr, args.steps, 0, events, lanes)
     w = PRECISIONS[precision][1]
     key = args.config if precision == "f32" else f"{args.config}_{precision}"
     rec = {
@@ -412,7 +413,7 @@ def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp:
                 break
             engine.run(total, snr, seed=20_000 + extra, group=rt.group)
             extra += 1
-        e2, _ = timed_steps(rt, engine, total, snr, args.steps, 30_000, None, args.lanes)
+        e2, _ = timed_steps(rt, engine, total, snr, args.steps, 30_000, None, lanes)
         rec["value_after_ramp"] = {"value": total * args.steps / e2, "ms_per_step": e2 / args.steps * 1e3,
                                    "extra_untimed_steps": extra, "ramp_seconds": args.ramp_seconds}
     return engine, rec
@@ -449,11 +450,12 @@ def measure_sweep(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory)
     N = cfg[0]
     engine = factory(cfg, precision)
     total = per_gpu * rt.world
-    engine.reserve(total, 2, group=rt.group, lanes=args.lanes)
+    lanes = args.lanes or 2
+    engine.reserve(total, 2, group=rt.group, lanes=lanes)
     grid = SWEEP_GRID
     for i in range(args.warmup):
         for p in engine.run_pipelined(total, grid, [50_000 + 100 * i + k for k in range(len(grid))], group=rt.group,
-                                      lanes=args.lanes):
+                                      lanes=lanes):
             p.result()
     events = None if rt.cpu else []
     rt.sync()
@@ -462,7 +464,7 @@ def measure_sweep(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory)
     t0 = time.perf_counter()
     snrs = grid * args.steps
     seeds = [1000 * st + k for st in range(args.steps) for k in range(len(grid))]
-    pend = engine.run_pipelined(total, snrs, seeds, group=rt.group, events=events, lanes=args.lanes)
+    pend = engine.run_pipelined(total, snrs, seeds, group=rt.group, events=events, lanes=lanes)
     errs = [p.result().bit_errors for p in pend]
     rt.sync()
     rt.barrier()
@@ -476,7 +478,9 @@ def measure_sweep(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory)
         "value": total * len(grid) * args.steps / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
         "dtype": PRECISIONS[precision][0],
-        "roofline": roofline(events, N, engine.bps, engine.cp, w, None),
+        # (with 2 lanes a kernel's events also span the other lane's overlapping kernel: the
+        # per-launch times, and so the roofline fraction, are upper / lower bounds)
+        "roofline": dict(roofline(events, N, engine.bps, engine.cp, w, None) or {}, lanes=lanes),
         "sweep": {"snr_db": grid, "ber": bers, "bits_per_point": nbits, "points": len(grid),
                   "symbols_per_point_per_step": total},
     }
@@ -505,8 +509,10 @@ def main():
     ap.add_argument("--sweep", action="store_true",
                     help="one step = the SNR sweep of BASELINE configs[2] (0..30 dB by 1 dB + 26..29 dB by 0.25 dB), "
                          "--symbols per GPU per point (default 1e5 x 1024/N)")
-    ap.add_argument("--lanes", type=int, default=1,
-                    help="HIP streams the timed runs alternate over (LinkEngine.run_pipelined)")
+    ap.add_argument("--lanes", type=int, default=None,
+                    help="HIP streams the timed runs alternate over (LinkEngine.run_pipelined); default 1, "
+                         "--sweep 2 (its 1e5-symbol points overlap a receiver with the next transmitter: "
+                         "1.02 -> 1.08e8 symbols/s, profiles/r04c_sweep_c*.json)")
     ap.add_argument("--ref-symbols", type=int, default=12000,
                     help="--sweep: reference-stream OFDM symbols per point near the BER 1e-4 crossing (26..29 dB)")
     args = ap.parse_args()

@@ -176,9 +176,6 @@ constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && L
 #ifndef OFDM_F64_RX_WAVES
 #define OFDM_F64_RX_WAVES 4
 #endif
-#ifndef OFDM_F64_RX_WIDE_EQ
-#define OFDM_F64_RX_WIDE_EQ 0
-#endif
 #ifndef OFDM_F64_FIR_BLOCK
 #define OFDM_F64_FIR_BLOCK 256
 #endif
@@ -258,15 +255,7 @@ __host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
 // QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves;
 // with an equaliser the 16 KB coefficient table beside 16 symbols' rows exceeds the LDS)
 template <int FB, int LOGN, int EQ, bool MV = false>
-constexpr bool f64_rx_wide() {
-    return (EQ == OFDM_EQ_NONE || OFDM_F64_RX_WIDE_EQ) && FB >= 6 && LOGN == 10 && !MV;
-}
-// (OFDM_F64_RX_WIDE_EQ: A/B of the 4-wave shape with an equaliser -- the coefficients buffer-loaded
-// after the FFT (rx_eq_late) instead of a 16 KB LDS table, which does not fit beside 16 symbols)
-template <typename R, int FB, int LOGN, int EQ>
-constexpr bool f64_rx_wide_eq() {
-    return OFDM_F64_RX_WIDE_EQ && sizeof(R) == 8 && EQ > OFDM_EQ_NONE && FB >= 6 && LOGN == 10;
-}
+constexpr bool f64_rx_wide() { return EQ == OFDM_EQ_NONE && FB >= 6 && LOGN == 10 && !MV; }
 // (the same for the adaptive RX at N = 2048 (config d) -- 128-thread workgroups
 // of one symbol at 2 waves per SIMD, instead of four symbols per 512-thread workgroup: RX 5.12 ->
 // 4.67 ms, step 10.11 -> 9.93 ms per 5e5 symbols, profiles/r03ad_ab.txt)
@@ -303,13 +292,11 @@ constexpr int rx_waves() {
 template <typename R, int FB, int LOGN, int EQ>
 constexpr bool eq_in_lds() {
     return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= (sizeof(R) == 8 ? 12 : OFDM_EQ_LDS_MAX_LOGN) &&
-           !f64_rx_solo<R, FB, LOGN>() && !f64_rx_wide_eq<R, FB, LOGN, EQ>();
+           !f64_rx_solo<R, FB, LOGN>();
 }
 // the lane's coefficients loaded after the FFT (in flight across the MMSE power reduction)
 template <typename R, int FB, int LOGN, int EQ>
-constexpr bool rx_eq_late() {
-    return (f64_rx_solo<R, FB, LOGN>() || f64_rx_wide_eq<R, FB, LOGN, EQ>()) && EQ > OFDM_EQ_NONE;
-}
+constexpr bool rx_eq_late() { return f64_rx_solo<R, FB, LOGN>() && EQ > OFDM_EQ_NONE; }
 // MMSE in complex128: the reciprocals of |H|^2 + nv of four elements from one v_rcp_f64 (+ two
 // Newton steps) and nine products (Montgomery's batch inversion; ~3 roundings more than one
 // reciprocal each, well inside the decision bracket's 8 u of equaliser arithmetic).  RX c 3.80 ->
@@ -317,11 +304,7 @@ constexpr bool rx_eq_late() {
 // complex128 throughput kernels exchange FFT data through rows of reals (fft_reg_split)
 template <typename R, int FB>
 constexpr bool split_rows() { return sizeof(R) == 8 && FB > 0; }
-#ifndef OFDM_F64_FIR_CROWS
-#define OFDM_F64_FIR_CROWS 0
-#endif
-template <typename R, int FB>
-constexpr bool f64_fir_crows() { return OFDM_F64_FIR_CROWS && sizeof(R) == 8 && FB > 0; }
+
 
 // Reference mode: stage OFDM symbol s's tx bits from the packed bytes of the run
 // (symbol s starts at bit s*bps, zeros past the end) as 32-bit words in W
@@ -469,10 +452,10 @@ __device__ __forceinline__ uint32_t nn_decide(cpx<R> v, const TxRxCommon& cm, in
 // FFT of one symbol in a fused kernel: complex128 throughput kernels exchange through a row of
 // reals (fft_reg_split), complex64 ones through the complex row with per-pass LDS twiddles, the
 // generic kernel with the two-level table and recurrence.
-template <typename R, int LOGN, bool INV, int FB, bool SPLIT = split_rows<R, FB>()>
+template <typename R, int LOGN, bool INV, int FB>
 __device__ __forceinline__ void fft_sym(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* row, const cpx<R>* tw,
                                         const cpx<R>* tt, int t) {
-    if constexpr (SPLIT)
+    if constexpr (split_rows<R, FB>())
         fft_reg_split<R, LOGN, INV, fast_tt<R, LOGN>()>(x, (R*)row, tw, tw + 64, t, tt);
     else
         fft_reg<R, LOGN, INV, (FB > 0)>(x, row, tw, tw + 64, t, tt);
@@ -512,10 +495,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     constexpr bool TT = uses_tt<R, LOGN, FB>();
     // complex128 flat and window-FIR TX: a row of reals (fft_reg_split)
     // (the window FIR passes its stream through the row of reals twice: real, then imaginary parts)
-    // (OFDM_F64_FIR_CROWS: the complex128 window-FIR TX on complex rows -- its FFT exchanges through
-    // complex samples, one write and one read per pass instead of two each; LDS for 2 waves/SIMD)
-    constexpr bool TX_SPLIT = split_rows<R, FB>() && !(LT > 0 && f64_fir_crows<R, FB>());
-    constexpr bool ROW_REAL = TX_SPLIT && LT >= 0;
+    constexpr bool ROW_REAL = split_rows<R, FB>() && LT >= 0;
     Carve cv(ofdm_smem);
     C* tw = cv.take<C>(TT ? 0 : 128);  // two-level twiddles (generic kernel, complex128 N > 1024)
     // throughput kernels: the LUT in static LDS at a link-time address, so an element's LUT read
@@ -645,7 +625,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     x[i] = v;
                 }
             }
-            if (!(flags & 2) && !scm) fft_sym<R, LOGN, true, FB, TX_SPLIT>(x, row, tw, tt, t);
+            if (!(flags & 2) && !scm) fft_sym<R, LOGN, true, FB>(x, row, tw, tt, t);
             // The prefix repeats samples k >= N - cp.  With cp <= TPS only the lane's last
             // element can be one of them (one loop-invariant compare); otherwise the compares
             // are made per symbol against an opaque copy of N - cp, so they are not hoisted
@@ -715,107 +695,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                 // free; offsets compile-time) -- 23 LDS reads instead of 2 L per output
                 static_assert(E == 16 && TPS >= 16, "window FIR geometry");
                 constexpr int WN = E + LT - 1;
-                if constexpr (sizeof(R) == 8 && !ROW_REAL) {
-                    // complex128 on complex rows (f64_fir_crows, 2 waves per SIMD): the whole
-                    // extended stream [tail | prefix | x] in the row at fir_pad(R0 + m) (lane stride
-                    // 17: conflict-free ds_read_b128 windows), written once; each lane streams its
-                    // window of 16 + LT - 1 samples through the Gauss sums of its 16 consecutive
-                    // outputs, 8 at a time; the 16 outputs leave through the row (fir_pad, read back
-                    // as t + TPS i): 4 synchronisations per symbol instead of 8.  Cyclic prefix only.
-                    static_assert(LT <= kWinTaps, "window FIR taps");
-                    C* crow = row;
-                    auto st16 = [&](int slot_, C v) { *(f64x2*)(crow + slot_) = f64x2{v.re, v.im}; };
-                    auto ld16 = [&](const C* p) { const f64x2 u = *(const f64x2*)p; return mk<R>(u.x, u.y); };
-                    const bool live = active && c >= 0;
-                    const bool store = live && yout && !(flags & 4);
-                    R hr[LT], c1[LT], c2[LT];
-#pragma unroll
-                    for (int q = 0; q < LT; ++q) {
-                        hr[q] = a.gtap[0][q];
-                        c1[q] = a.gtap[1][q];
-                        c2[q] = a.gtap[2][q];
-                    }
-                    int to = t, cpo = cp, lo = L;
-                    asm volatile("" : "+v"(to), "+s"(cpo), "+s"(lo));
-                    const int Ao = (cpo + 15) & ~15, Ro = Ao - cpo + LT - 1;
-                    sym_sync<TPS>();  // the last FFT pass has read the row
-                    {
-                        const int bx = fir_pad(Ro + cpo + to);  // stream sample cp + t + TPS i
-                        static_for<0, E>([&](auto I) { st16(bx + TPS * I + (TPS * I >> 4), x[I]); });
-                    }
-                    if (to >= TPS - cpo) st16(fir_pad(Ro + to - (TPS - cpo)), x[E - 1]);  // cyclic prefix
-                    if (to < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
-                        const int z = to - (LT - lo);
-                        st16(fir_pad(Ro - (LT - 1) + to), z < 0 ? mk<R>(0, 0) : tl[z]);
-                    }
-                    sym_sync<TPS>();
-                    // this symbol's tail for the next one, from the registers
-                    if (to >= TPS - (lo - 1)) tl[to - (TPS - (lo - 1))] = active ? x[E - 1] : mk<R>(0, 0);
-                    const C* wb = crow + (Ao + (Ao >> 4) + 17 * to);
-                    R pys = 0;
-                    if (live && to < cpo) {  // prefix-region output m = t: power only (noise/models.py:14)
-                        R pT = 0, pU = 0, pV = 0;
-#pragma unroll
-                        for (int l = 0; l < LT; ++l) {
-                            const C e = ld16(crow + fir_pad(Ro + to - l));
-                            pT = __builtin_fma(hr[l], e.re + e.im, pT);
-                            pU = __builtin_fma(c1[l], e.im, pU);
-                            pV = __builtin_fma(c2[l], e.re, pV);
-                        }
-                        const R pr = pT - pU, pi = pT + pV;
-                        pys = __builtin_fma(pr, pr, pys);
-                        pys = __builtin_fma(pi, pi, pys);
-                    }
-                    C yo[E];
-                    static_for<0, 2>([&](auto HH) {
-                        constexpr int h = HH;
-                        R T[8], U[8], V[8];
-                        constexpr int W0 = 8 * h, WH = 8 + LT - 1;
-                        C ring[3];
-                        ring[0] = ld16(wb + (W0 + (W0 >> 4)));
-                        ring[1] = ld16(wb + ((W0 + 1) + ((W0 + 1) >> 4)));
-                        static_for<0, WH>([&](auto Wl) {
-                            constexpr int W = W0 + Wl;
-                            if constexpr (Wl + 2 < WH) ring[(Wl + 2) % 3] = ld16(wb + ((W + 2) + ((W + 2) >> 4)));
-                            const C e = ring[Wl % 3];
-                            const R sw = e.re + e.im;
-                            static_for<0, LT>([&](auto Q) {
-                                constexpr int j = Wl - (LT - 1) + Q;  // output 8 h + j
-                                if constexpr (j >= 0 && j < 8) {
-                                    if constexpr (Q == LT - 1) {
-                                        T[j] = hr[Q] * sw;
-                                        U[j] = c1[Q] * e.im;
-                                        V[j] = c2[Q] * e.re;
-                                    } else {
-                                        T[j] = __builtin_fma(hr[Q], sw, T[j]);
-                                        U[j] = __builtin_fma(c1[Q], e.im, U[j]);
-                                        V[j] = __builtin_fma(c2[Q], e.re, V[j]);
-                                    }
-                                }
-                            });
-                            __builtin_amdgcn_sched_barrier(0);
-                        });
-#pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            yo[8 * h + j] = mk<R>(T[j] - U[j], T[j] + V[j]);
-                            pys = __builtin_fma(yo[8 * h + j].re, yo[8 * h + j].re, pys);
-                            pys = __builtin_fma(yo[8 * h + j].im, yo[8 * h + j].im, pys);
-                        }
-                    });
-                    sym_sync<TPS>();  // every window is read: the outputs take the row
-                    static_for<0, E>([&](auto J) { st16(17 * to + J, yo[J]); });  // fir_pad(16 t + j)
-                    sym_sync<TPS>();
-                    if (store) {
-                        C* ys = yout + sl * N;
-                        gptr<C> yg = TPS >= 64 ? uniform_ptr(ys) : (gptr<C>)ys;
-                        const C* rb = crow + fir_pad(to);
-#pragma unroll
-                        for (int i = 0; i < E; ++i)
-                            st_stream<TX_NT>(lane_ptr(yg, (uint32_t)(to + TPS * i)), ld16(rb + TPS * i + (TPS * i >> 4)));
-                    }
-                    if (live) fx_accum((R)pys, pq0, pq1);
-                    sym_sync<TPS>();
-                } else if constexpr (sizeof(R) == 8) {
+                if constexpr (sizeof(R) == 8) {
                     // complex128: the FIR runs over the symbol in two halves of N / 2 kept samples,
                     // through the symbol's row of reals used as complex samples, one pad slot per 8
                     // (wfir_slot).  Half h holds the stream samples m in [cp + h N/2 - (LT-1),

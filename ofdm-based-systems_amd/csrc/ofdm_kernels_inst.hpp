@@ -176,17 +176,9 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
         if constexpr (sizeof(R) == 8) {
             // complex128: the row of reals carries half a symbol's stream as complex samples, half 0's
             // m in [-(LT-1), cp + N/2) at wfir_slot(A8 - cp + LT - 1 + m), and N / 2 transposed outputs
-            // (complex rows: the same counts in complex elements)
-            if constexpr (f64_fir_crows<R, FB>()) {
-                // complex rows: the whole stream at fir_pad(R0 + m) and the N outputs at fir_pad(k)
-                const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
-                a.slot = std::max(a.slot, fir_pad(R0 + (1 << LOGN) + a.c.cp) + 1);
-                a.slot = std::max(a.slot, fir_pad((1 << LOGN) - 1) + 1);
-            } else {
-                const int A8 = (a.c.cp + 7) & ~7;
-                a.slot = std::max(a.slot, 2 * (wfir_slot(A8 + (1 << LOGN) / 2 + LT - 2) + 1));
-                a.slot = std::max(a.slot, 2 * (wfir_slot((1 << LOGN) / 2 - 1) + 1));
-            }
+            const int A8 = (a.c.cp + 7) & ~7;
+            a.slot = std::max(a.slot, 2 * (wfir_slot(A8 + (1 << LOGN) / 2 + LT - 2) + 1));
+            a.slot = std::max(a.slot, 2 * (wfir_slot((1 << LOGN) / 2 - 1) + 1));
         } else {
             // window FIR row: stream samples [-(LT-1), N+cp) at fir_pad(R0 + m)
             const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
@@ -195,8 +187,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     }
     const size_t sm = smem_tx<R>(LOGN, BLK, FB > 0 ? 0 : a.c.lut_len, a.c.words_per_sym, a.L, a.slot,
                                  uses_tt<R, LOGN, FB>() ? tt_size(LOGN) : 0, FB > 0 && LT > 0,
-                                 FB == 1 ? (size_t)4 << LOGN : 0, FB > 0,
-                                 split_rows<R, FB>() && LT >= 0 && !(LT > 0 && f64_fir_crows<R, FB>()));
+                                 FB == 1 ? (size_t)4 << LOGN : 0, FB > 0, split_rows<R, FB>() && LT >= 0);
     if constexpr (FB > 0) {
         if (sm + tx_static_lds<R, FB, LT>() > kLdsPerCu) return tx_launch<R, LOGN, 0, -1>(a0, grid, s);
     }
@@ -217,8 +208,7 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     if (a.L == 1 && !a.c.zpad) return tx_launch<R, LOGN, FB, 0>(a, grid, s);
     if constexpr (LOGN >= 8) {
         // the complex64 register window assumes a cyclic prefix; the complex128 one takes zero padding
-        // (on rows of reals)
-        if (a.c.cp <= TPS && (!a.c.zpad || (sizeof(R) == 8 && !f64_fir_crows<R, FB>()))) {
+        if (a.c.cp <= TPS && (!a.c.zpad || sizeof(R) == 8)) {
             if (a.L <= 4) return tx_launch<R, LOGN, FB, 4>(a, grid, s);
             if (a.L <= 8) return tx_launch<R, LOGN, FB, 8>(a, grid, s);
         }

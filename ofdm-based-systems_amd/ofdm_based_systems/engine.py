@@ -263,9 +263,9 @@ class LinkEngine:
     def lane_streams(self, lanes: int) -> list:
         """The current stream and lanes - 1 more, kept per engine (their allocator pools persist:
         reserve() fills them before a timed region)."""
-        cur = torch.cuda.current_stream()
         if lanes <= 1 or self.device().type != "cuda":
-            return [cur]
+            return [None]
+        cur = torch.cuda.current_stream()
         extra = getattr(self, "_lanes", [])
         while len(extra) < lanes - 1:
             extra.append(torch.cuda.Stream())
@@ -311,7 +311,7 @@ class LinkEngine:
             return [self.run_async(n_sym, q, seed=s, group=group, events=events, y_budget=y_budget)
                     for s, q in zip(seeds, snrs)]
 
-        lane_list = self.lane_streams(lanes) if lanes > 1 else None
+        lane_list = self.lane_streams(lanes) if lanes > 1 and dev.type == "cuda" else None
 
         def on(k):
             """Context of run k's lane (the current stream when not alternating)."""
