@@ -737,6 +737,14 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     // symbol loop they were ~20 loop-invariant registers, spilled to scratch
                     int to = t, cpo = cp, lo = L;
                     asm volatile("" : "+v"(to), "+s"(cpo), "+s"(lo));
+                    if (c < 0 && !zp) {
+                        // a group's regenerated predecessor: only its tail is needed, the last
+                        // L - 1 samples of x (registers); no FIR, no stores
+                        sym_sync<TPS>();  // the previous symbol's FIR has read the old tail
+                        if (to >= TPS - (lo - 1)) tl[to - (TPS - (lo - 1))] = active ? x[E - 1] : mk<R>(0, 0);
+                        sym_sync<TPS>();
+                        continue;
+                    }
                     const int so = zp ? 0 : cpo;  // stream sample of x[0]
                     const int A8 = (so + 7) & ~7;
                     R pys = 0;
