@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--ref-symbols", type=int, default=12_000, help="reference-stream OFDM symbols per SNR point")
     ap.add_argument("--precision", default="f32", choices=("f32", "f64"),
                     help="arithmetic of the throughput-mode kernels (complex64 / complex128)")
+    ap.add_argument("--grid", default="", help="comma-separated SNR points (dB) instead of the config's grid")
     ap.add_argument("--ref-min-snr", type=float, default=20.0,
                     help="below this SNR the reference-stream path runs --ref-symbols/8 (errors are plentiful)")
     args = ap.parse_args()
@@ -83,6 +84,8 @@ def main():
 
     PREC = B.OFDM_F32 if args.precision == "f32" else B.OFDM_F64
     N, M, ch, eq, grid = CONFIGS[args.config]
+    if args.grid:
+        grid = [float(x) for x in args.grid.split(",")]
     grid = sorted(set(grid))
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
     cp = len(h) - 1

@@ -1,5 +1,7 @@
 set -o pipefail
-TAG=r04d NO_BENCH=1 tools/gpu_session.sh || exit $?
-timeout -k 10 400 python bench.py > gpurun_out/r04d_bench_b.json 2> gpurun_out/r04d_bench_b.err; echo bench-b rc=$?; tail -c 1500 gpurun_out/r04d_bench_b.json
-for cfg in c d e; do timeout -k 10 300 python bench.py --config $cfg --no-cpu-baseline > gpurun_out/r04d_bench_$cfg.json 2> gpurun_out/r04d_bench_$cfg.err; echo bench-$cfg rc=$?; python -c "import json; d=json.load(open('gpurun_out/r04d_bench_$cfg.json')); print('$cfg', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['avg_launch_ms'], d.get('ber_vs_reference',{}).get('delta_db'))"; done
-timeout -k 10 400 python bench.py --config c --sweep > gpurun_out/r04d_sweep.json 2> gpurun_out/r04d_sweep.err; echo sweep rc=$?; python -c "import json; d=json.load(open('gpurun_out/r04d_sweep.json')); print('sweep', d['value'], d['ms_per_step'], d.get('delta_db_at_1e-4'), d.get('cpu_baseline',{}).get('value'))"
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+for cfg in b c d e; do
+  out=gpurun_out/prof_r04f_${cfg}_f64; mkdir -p $out
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o trace --output-format csv -- python3 bench.py --config $cfg --precision f64 --steps 30 --warmup 2 --no-cpu-baseline --no-ber-check --no-variant > $out/trace.log 2>&1
+  rc=$?; echo "$cfg trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
