@@ -135,6 +135,12 @@ __device__ __forceinline__ T buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff,
     static_assert(sizeof(T) == 16, "16-byte element");
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, NT ? 2 : 0));
 }
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <typename T, bool NT = false>
+__device__ __forceinline__ void buf_store16(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    static_assert(sizeof(T) == 16, "16-byte element");
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, (int)voff, (int)soff, NT ? 2 : 0);
+}
 
 // complex128 multipath TX of square QAM (the plan sends only separable LUTs to the throughput
 // kernels): map through the two axis tables instead of the complex LUT (TX c 5.13 -> 5.12, e 5.26
@@ -197,13 +203,13 @@ constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && L
 #define OFDM_TX_BIG_WFIR_WAVES 3
 #endif
 // LDS of the complex128 FIR TX at blk threads (upper estimate of its Carve sequence, smem_tx):
-// FIR rows -- window FIR: half a symbol's stream as complex samples, wfir_slot(N/2 + 48) + 1 of
+// FIR rows -- window FIR: half a symbol's stream as complex samples, wfir_in(N/2 + 48) + 1 of
 // them (cp <= 32), or the FFT's N + N/16 reals if more; the run-time-tap FIR: fir_pad(N + 32) + 1
 // complex -- and the 7 complex tail samples per symbol, per-pass twiddles, the static LUT
 // (adaptive: the 512-entry pool and the per-subcarrier table), taps
 constexpr int f64_fir_lds(int fb, int logn, int blk, bool real_rows) {
     const int n = 1 << logn, tps = logn < 4 ? 1 : n >> 4, spb = blk / tps;
-    const int fir = (n + 32) + ((n + 32) >> 4) + 1, half = 2 * (n / 2 + 48 + ((n / 2 + 48) >> 3) + 1);
+    const int fir = (n + 32) + ((n + 32) >> 4) + 1, half = 2 * (n / 2 + 48 + ((n / 2 + 48 + 7) >> 3) + 1);
     const int padn = n + (n >> 4);
     const int rows = spb * ((real_rows ? (half > padn ? half : padn) * 8 : fir * 16) + 7 * 16);
     const int tt = tt_size(logn) * 16;
@@ -239,9 +245,17 @@ constexpr int tx_waves() {
 }
 // padded FIR row index of the throughput multipath TX: one slot per 16 elements
 __host__ __device__ constexpr int fir_pad(int i) { return i + (i >> 4); }
-// complex128 window-FIR TX: slot of output kk (of N / 2) in the row while it is transposed
-// for the store: one pad slot per 8, so the lanes' stride-8 writes fall on distinct banks
-__host__ __device__ constexpr int wfir_slot(int kk) { return kk + (kk >> 3); }
+// complex128 window-FIR TX, LDS slots (16 bytes) of the half-symbol row.  Stream phase: stream
+// index kk at wfir_in(kk) -- one pad slot per 8, placed so that the FFT elements (kk = LT - 1 +
+// t + TPS i mod 8: every 8 lanes one aligned run) are written without a pad inside an 8-lane
+// group, and the lanes' windows (kk = 8 t + W) read at lane stride 9.  Output phase: output kk at
+// wfir_out(kk), an XOR swizzle of the 8-slot runs -- the lanes' runs of 8 outputs are written to
+// distinct banks and the stores' reads (kk = t + TPS i) hit 16 distinct 4-bank sets per
+// ds_read_b128 lane group.  Against wfir_slot (kk + kk / 8) for both phases: no bank conflicts
+// (SQ_LDS_BANK_CONFLICT 197 cycles per config-c symbol, tools/lds_banks.py --fir models 192).
+__host__ __device__ constexpr int wfir_ioff(int lt) { return (9 - lt) & 7; }
+__host__ __device__ constexpr int wfir_in(int kk, int lt) { return kk + ((kk + wfir_ioff(lt)) >> 3); }
+__host__ __device__ constexpr int wfir_out(int kk) { return (kk & ~7) | ((kk ^ (kk >> 3)) & 7); }
 // complex128 RX of fixed QAM at N = 4096 (config e): one symbol per 256-thread workgroup at 3 waves
 // per SIMD, the equaliser coefficients read from the plan's table after the FFT (rx_eq_late)
 // instead of a 64 KB LDS copy per workgroup -- with the copy, two symbols per 512-thread workgroup
@@ -634,7 +648,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
             asm volatile("" : "+s"(ncp));
             auto prefix_sum = [&](auto&& pw) -> R {
                 if (zp) return (R)0;  // the zero guard adds no power
-                if (cp <= TPS) return t >= TPS - cp ? pw(E - 1) : (R)0;
+                if (WFIR || cp <= TPS) return t >= TPS - cp ? pw(E - 1) : (R)0;  // (window FIR: cp <= TPS)
                 R acc = 0;
 #pragma unroll
                 for (int i = 0; i < E; ++i)
@@ -698,8 +712,8 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                 if constexpr (sizeof(R) == 8) {
                     // complex128: the FIR runs over the symbol in two halves of N / 2 kept samples,
                     // through the symbol's row of reals used as complex samples, one pad slot per 8
-                    // (wfir_slot).  Half h holds the stream samples m in [cp + h N/2 - (LT-1),
-                    // cp + (h+1) N/2) at wfir_slot(B_h + m) -- half 0 from m = -(LT-1): the previous
+                    // (wfir_in).  Half h holds the stream samples m in [cp + h N/2 - (LT-1),
+                    // cp + (h+1) N/2) at wfir_in(B_h + m) -- half 0 from m = -(LT-1): the previous
                     // symbol's tail and the prefix region too -- and lane t computes the 8
                     // consecutive kept samples k = h N/2 + 8 t + j from a window of 8 + LT - 1
                     // complex samples (ds_read_b128 at lane stride 9: conflict free), streamed one
@@ -711,8 +725,9 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     // TxArgs::gtap, zero past L).  Live at once: half a symbol's elements, 24
                     // accumulators and the streamed sample -- against two whole windows of reals and
                     // 16 outputs' sums when the row carried the real and then the imaginary parts.
-                    // The outputs leave through the row (kk = 8 t + j at wfir_slot(kk), read back as
-                    // kk = t + TPS i): lanes 8 m .. 8 m + 7 store one whole 128-byte line.
+                    // The outputs leave through the row (kk = 8 t + j at wfir_out(kk), read back as
+                    // kk = t + TPS i) and buffer stores: lanes 8 m .. 8 m + 7 store one whole
+                    // 128-byte line.
                     // Zero padding (prefix/models.py:55-67, the stream [x | 0 ... 0]): x starts at
                     // stream sample 0 instead of cp, every one of the N + cp outputs is stored
                     // (ystride N + cp: the receiver overlap-adds the guard), the guard outputs
@@ -751,14 +766,14 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     static_for<0, 2>([&](auto HH) {
                         constexpr int h = HH;
                         constexpr int NH = N / 2;
-                        // stream sample m at wfir_slot(B + m); the lanes' windows start at Ah + 8 t
+                        // stream sample m at wfir_in(B + m); the lanes' windows start at Ah + 8 t
                         const int Ah = h == 0 ? A8 : 0;
                         const int B = Ah - so - h * NH + (LT - 1);
                         sym_sync<TPS>();  // the FFT's last pass / the previous half's stores have read the row
                         // this half's elements: kept k = t + TPS i (stream cp + k) for k in
                         // [h N/2 - (LT-1), (h+1) N/2); TPS i = N/2 at i = 8
-                        // (TPS i = 0 mod 8: wfir_slot(b + TPS i) = wfir_slot(b) + 9 TPS i / 8)
-                        const int bx = wfir_slot(B + so + to);
+                        // (TPS i = 0 mod 8: wfir_in(b + TPS i) = wfir_in(b) + 9 TPS i / 8)
+                        const int bx = wfir_in(B + so + to, LT);
                         static_for<0, E>([&](auto I) {
                             constexpr int i = I;
                             constexpr int off = 9 * TPS * i / 8;
@@ -769,10 +784,10 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             }
                         });
                         if constexpr (h == 0) {
-                            if (!zp && to >= TPS - cpo) st16(wfir_slot(B + to - (TPS - cpo)), x[E - 1]);  // cyclic prefix
+                            if (!zp && to >= TPS - cpo) st16(wfir_in(B + to - (TPS - cpo), LT), x[E - 1]);  // cyclic prefix
                             if (to < LT - 1) {  // stream samples -(LT-1) .. -1: zeros, then the previous tail
                                 const int z = to - (LT - lo);
-                                st16(wfir_slot(B - (LT - 1) + to), z < 0 ? mk<R>(0, 0) : tl[z]);
+                                st16(wfir_in(B - (LT - 1) + to, LT), z < 0 ? mk<R>(0, 0) : tl[z]);
                             }
                         }
                         sym_sync<TPS>();
@@ -785,21 +800,23 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             // below N, guard zeros from N on
                             if (zp && to < lo - 1) {
                                 const int m = N + cpo - (lo - 1) + to;
-                                tl[to] = (active && m < N) ? ld16(crow + wfir_slot(B + m)) : mk<R>(0, 0);
+                                tl[to] = (active && m < N) ? ld16(crow + wfir_in(B + m, LT)) : mk<R>(0, 0);
                             }
                         }
                         // every lane streams its window, live or not (under the live condition the
                         // accumulators would be conditionally defined and spill)
-                        const C* wb = crow + (wfir_slot(Ah) + 9 * to);
+                        // (wfir_in(Ah + 8 t + W) = wfir_in(Ah) + 9 t + W + (W + ioff) / 8)
+                        const C* wb = crow + (wfir_in(Ah, LT) + 9 * to);
+                        constexpr int IOFF = wfir_ioff(LT);
                         R T[8], U[8], V[8];
                         // the window streamed two samples ahead of its use; the scheduling barrier
                         // keeps the compiler from issuing all 8 + LT - 1 reads at once (a whole
                         // window of live registers at the peak of the kernel)
                         C ring[3];
-                        ring[0] = ld16(wb);
-                        ring[1] = ld16(wb + 1);
+                        ring[0] = ld16(wb + (IOFF >> 3));
+                        ring[1] = ld16(wb + (1 + ((1 + IOFF) >> 3)));
                         static_for<0, WH>([&](auto W) {
-                            if constexpr (W + 2 < WH) ring[(W + 2) % 3] = ld16(wb + ((W + 2) + ((W + 2) >> 3)));
+                            if constexpr (W + 2 < WH) ring[(W + 2) % 3] = ld16(wb + ((W + 2) + ((W + 2 + IOFF) >> 3)));
                             const C e = ring[W % 3];
                             const R sw = e.re + e.im;
                             static_for<0, LT>([&](auto Q) {  // tap Q of output j
@@ -826,7 +843,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
 #pragma unroll
                                 for (int l = 1; l < LT; ++l) {
                                     if (l <= to) continue;
-                                    const C e = ld16(crow + wfir_slot(B + N + to - l));
+                                    const C e = ld16(crow + wfir_in(B + N + to - l, LT));
                                     pT = __builtin_fma(hr[l], e.re + e.im, pT);
                                     pU = __builtin_fma(c1[l], e.im, pU);
                                     pV = __builtin_fma(c2[l], e.re, pV);
@@ -842,7 +859,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                                 R pT = 0, pU = 0, pV = 0;
 #pragma unroll
                                 for (int l = 0; l < LT; ++l) {
-                                    const C e = ld16(crow + wfir_slot(B + to - l));
+                                    const C e = ld16(crow + wfir_in(B + to - l, LT));
                                     pT = __builtin_fma(hr[l], e.re + e.im, pT);
                                     pU = __builtin_fma(c1[l], e.im, pU);
                                     pV = __builtin_fma(c2[l], e.re, pV);
@@ -858,17 +875,30 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             const C yv = mk<R>(T[j] - U[j], T[j] + V[j]);
                             pys = __builtin_fma(yv.re, yv.re, pys);
                             pys = __builtin_fma(yv.im, yv.im, pys);
-                            st16(9 * to + j, yv);  // wfir_slot(8 t + j)
+                            st16(8 * to + (j ^ (to & 7)), yv);  // wfir_out(8 t + j)
                         }
                         sym_sync<TPS>();
                         if (store) {
-                            // (the symbol's base is wave-uniform when a wave holds one symbol)
+                            // global stores off two wave-uniform bases (elements i < 4 and i >= 4),
+                            // the lane's 32-bit byte offset in one VGPR and element i's in the
+                            // instruction's offset field (per-element 64-bit VGPR addresses were
+                            // loop-invariant registers).  (Buffer stores with SGPR offsets here
+                            // corrupted the last store's low data dword on gfx950: the compiler
+                            // inserts no wait state between such a store and a VALU write of its
+                            // data VGPRs.)
                             C* yh = yout + sl * ystride + h * NH;
-                            gptr<C> yg = TPS >= 64 ? uniform_ptr(yh) : (gptr<C>)yh;
-                            const C* rb = crow + wfir_slot(to);
+                            const C* rb = crow + wfir_out(to);
 #pragma unroll
-                            for (int i = 0; i < 8; ++i)
-                                st_stream<TX_NT>(lane_ptr(yg, (uint32_t)(to + TPS * i)), ld16(rb + 9 * TPS * i / 8));
+                            for (int i = 0; i < 8; ++i) {
+                                // (TPS = 0 mod 64: wfir_out(t + TPS i) = wfir_out(t) + TPS i)
+                                const C* ri = TPS % 64 == 0 ? rb + TPS * i : crow + wfir_out(to + TPS * i);
+                                if constexpr (TPS >= 64) {
+                                    gptr<C> yg = uniform_ptr(yh + (i >> 2) * 4 * TPS);
+                                    st_stream<TX_NT>(lane_ptr(yg, (uint32_t)to) + (i & 3) * TPS, ld16(ri));
+                                } else {
+                                    st_stream<TX_NT>((gptr<C>)yh + to + TPS * i, ld16(ri));
+                                }
+                            }
                         }
                     });
                     if (live) fx_accum((R)pys, pq0, pq1);

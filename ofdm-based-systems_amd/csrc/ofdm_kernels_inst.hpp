@@ -175,10 +175,10 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     if (FB > 0 && LT > 0) {
         if constexpr (sizeof(R) == 8) {
             // complex128: the row of reals carries half a symbol's stream as complex samples, half 0's
-            // m in [-(LT-1), cp + N/2) at wfir_slot(A8 - cp + LT - 1 + m), and N / 2 transposed outputs
+            // m in [-(LT-1), cp + N/2) at wfir_in(A8 - cp + LT - 1 + m), and N / 2 transposed outputs
             const int A8 = (a.c.cp + 7) & ~7;
-            a.slot = std::max(a.slot, 2 * (wfir_slot(A8 + (1 << LOGN) / 2 + LT - 2) + 1));
-            a.slot = std::max(a.slot, 2 * (wfir_slot((1 << LOGN) / 2 - 1) + 1));
+            a.slot = std::max(a.slot, 2 * (wfir_in(A8 + (1 << LOGN) / 2 + LT - 2, LT) + 1));
+            a.slot = std::max(a.slot, 2 * (wfir_out((1 << LOGN) / 2 - 1) + 1));
         } else {
             // window FIR row: stream samples [-(LT-1), N+cp) at fir_pad(R0 + m)
             const int A = (a.c.cp + 15) & ~15, R0 = A - a.c.cp + LT - 1;
