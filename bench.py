@@ -494,7 +494,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--symbols", type=int, default=0,
                     help="OFDM symbols per GPU per step (default 1e6 x 1024/N)")
-    ap.add_argument("--config", default="b", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="BASELINE config (default b; with --sweep, c: the sweep BASELINE configs[2] names)")
     ap.add_argument("--precision", default="f64", choices=sorted(PRECISIONS),
                     help="arithmetic of the headline line (f64 = complex128, the reference's)")
     ap.add_argument("--no-variant", action="store_true", help="skip the complex64 companion run")
@@ -516,6 +517,8 @@ def main():
     ap.add_argument("--ref-symbols", type=int, default=12000,
                     help="--sweep: reference-stream OFDM symbols per point near the BER 1e-4 crossing (26..29 dB)")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "c" if args.sweep else "b"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args.gpus))

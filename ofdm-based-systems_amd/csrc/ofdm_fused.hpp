@@ -1214,7 +1214,9 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     // kept channel samples of local symbol sl.  Past the end the wave reads the last symbol
     // again (its results are neither counted nor stored): an unconditional load, where zeroing
     // the 16 elements cost 32 v_mov_b64 per symbol in complex128.  Zeros when ablated.
-    constexpr bool RX_BUF = F64_FAST && TPS == 64;
+    // (symbols of 2 / 4 waves too, N = 2048 / 4096: the row base is wave-uniform when TPS >= 64;
+    // RX d 4.67 -> 4.63, e 4.15 -> 4.12 ms per step, profiles/r04h_ab_rxbuf_ch64.txt)
+    constexpr bool RX_BUF = F64_FAST && TPS >= 64;
     auto load_sym = [&](int64_t sl, C (&dst)[E]) {
         const C* ys = (const C*)a.y + (sl < cm.n_sym ? sl : cm.n_sym - 1) * ystride;
         if (RX_BUF && !(flags & 16)) {

@@ -3,7 +3,7 @@
 ofdm_launch.hpp).  Each variant runs back-to-back steps for --seconds while rocm-smi is
 sampled; the first 0.5 s (clock ramp) is not sampled.
 
-    python tools/power_probe.py [--config b] [--seconds 3] [--only full,rx_only,...]
+    python tools/power_probe.py [--config b] [--precision f64] [--seconds 3] [--only full,rx_only,...]
 
 The switches exist only in the ablation build of the library:
     make -C ofdm-based-systems_amd VARIANT=ablate EXTRA=-DOFDM_ABLATION=1
@@ -63,12 +63,14 @@ def main():
     ap.add_argument("--seconds", type=float, default=3.0)
     ap.add_argument("--symbols", type=int, default=1_000_000)
     ap.add_argument("--only", default="")
+    ap.add_argument("--precision", default="f32", choices=("f32", "f64"))
     args = ap.parse_args()
     N, M, ch, ratio, eq_name, snr, _ = CONFIGS[args.config]
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
     cp = int(ratio * (len(h) - 1))
     eq = {"NONE": B.EQ_NONE, "ZF": B.EQ_ZF, "MMSE": B.EQ_MMSE}[eq_name]
-    eng = LinkEngine(N, cp, h, eq, [QAMConstellationMapper(M).constellation], None, B.OFDM_F32)
+    eng = LinkEngine(N, cp, h, eq, [QAMConstellationMapper(M).constellation], None,
+                     B.OFDM_F64 if args.precision == "f64" else B.OFDM_F32)
     eng.run(1000, snr, seed=1)
     names = [n for n in VARIANTS if not args.only or n in args.only.split(",")]
     res = {}
@@ -111,7 +113,7 @@ def main():
         print(name, json.dumps(res[name]), flush=True)
     os.environ.pop("OFDM_ABLATE_TX")
     os.environ.pop("OFDM_ABLATE_RX")
-    print(json.dumps({"config": args.config, "symbols": args.symbols, "variants": res}))
+    print(json.dumps({"config": args.config, "precision": args.precision, "symbols": args.symbols, "variants": res}))
 
 
 if __name__ == "__main__":

@@ -1,7 +1,9 @@
+#!/bin/bash
+# steady-state traces + PMC of the final build (30 timed steps after the bench's clock ramp)
 set -o pipefail
-export TMPDIR=/tmp PYTHONUNBUFFERED=1
-for cfg in b c d e; do
-  out=gpurun_out/prof_r04f_${cfg}_f64; mkdir -p $out
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o trace --output-format csv -- python3 bench.py --config $cfg --precision f64 --steps 30 --warmup 2 --no-cpu-baseline --no-ber-check --no-variant > $out/trace.log 2>&1
-  rc=$?; echo "$cfg trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+for c in b c d e; do
+  PROF_STEPS=30 bash tools/profile.sh r04j_${c}_f64 --config $c --precision f64 --warmup 2 --ramp-seconds 0.25 > gpurun_out/r04j_prof_$c.txt 2>&1
+  rc=$?; echo "$c rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/r04j_prof_$c.txt; exit $rc; }
+  grep -h "k_tx\|k_rx" gpurun_out/prof_r04j_${c}_f64/trace/*kernel_stats.csv | cut -c1-120
 done
