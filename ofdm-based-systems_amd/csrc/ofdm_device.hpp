@@ -393,6 +393,10 @@ __device__ __forceinline__ void sym_sync() {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     } else {
+        // LDS writes issued as inline assembly (OFDM_SPLIT_WRITE_B64) are not
+        // tracked by the compiler's wait-count pass, which drops the barrier's lgkmcnt(0) when it
+        // sees no LDS operation of its own in flight: wait here, so the other waves read them
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __syncthreads();
     }
 }
@@ -472,6 +476,40 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
     if constexpr (!LAST) sym_sync<G::TPS>();
 }
 
+// OFDM_SPLIT_READ_B64: the split exchange's reads as single ds_read_b64 (inline assembly) instead of
+// the compiler's ds_read2_b64 pairs
+#ifndef OFDM_SPLIT_READ_B64
+#define OFDM_SPLIT_READ_B64 1
+#endif
+// OFDM_SPLIT_WRITE_B64: the exchange's writes as single ds_write_b64 (inline assembly) instead of the
+// compiler's ds_write2_b64 pairs (c 1.196 -> 1.218e8, d 5.43 -> 5.51e7 symbols/s,
+// profiles/r04l_ab_orderparams_writeb64.txt)
+#ifndef OFDM_SPLIT_WRITE_B64
+#define OFDM_SPLIT_WRITE_B64 1
+#endif
+// 32-bit LDS address of a pointer into __shared__ memory
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(const T* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) T*)p;
+}
+// one ds_read_b64 at LDS byte address la + OFF (inline assembly: no lgkmcnt accounting by the compiler)
+template <int OFF>
+__device__ __forceinline__ void ds_read_b64_at(double& d, uint32_t la) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(d) : "v"(la), "i"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void ds_write_b64_at(uint32_t la, double d) {
+    asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(la), "v"(d), "i"(OFF) : "memory");
+}
+// s_waitcnt lgkmcnt(0) that the 16 values read by inline-assembly LDS loads pass through
+__device__ __forceinline__ void lgkm_wait16(double (&u)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
+                   "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
+                 :
+                 : "memory");
+}
+
 // complex128 throughput kernels: the transposes between passes go through a row of N doubles,
 // real parts first, then imaginary parts -- half the LDS of a complex row per symbol, so twice
 // as many symbols (waves) fit a CU at the register budget complex128 needs.  Every pass takes
@@ -530,7 +568,17 @@ __device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb,
             for (int q = 0; q < NB; ++q) {
                 const int j = t + q * G::TPS;
                 const int idx = ((j >> LOGNS) << (LOGNS + LOGR)) + (j & (NS - 1));
-                if constexpr (NS % 16 == 0) {
+                if constexpr (sizeof(R) == 8 && OFDM_SPLIT_WRITE_B64 && (NS % 16 == 0 || NS == 1)) {
+                    // one ds_write_b64 per element (the compiler's ds_write2_b64 pairs cost 13 LDS
+                    // cycles per KB against 12 for two single writes); NS = 1: idx = 0 mod 16, so
+                    // pad(idx + r) = pad(idx) + r
+                    const uint32_t la = lds_addr(rb + pad(idx));
+                    static_for<0, RAD>([&](auto Rr) {
+                        constexpr int C = Rr * NS;
+                        constexpr int off = 8 * (NS == 1 ? C : C + (C >> 4));
+                        ds_write_b64_at<off>(la, im ? v[q][Rr].im : v[q][Rr].re);
+                    });
+                } else if constexpr (NS % 16 == 0) {
                     const int pi = pad(idx);
                     static_for<0, RAD>([&](auto Rr) { rb[pad_plus<Rr * NS>(pi)] = im ? v[q][Rr].im : v[q][Rr].re; });
                 } else {
@@ -540,7 +588,23 @@ __device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb,
             }
         };
         auto get = [&](bool im) {
-            if constexpr (G::TPS % 16 == 0) {
+            if constexpr (G::TPS % 16 == 0 && sizeof(R) == 8 && OFDM_SPLIT_READ_B64) {
+                // one ds_read_b64 per element: the compiler pairs the reads into ds_read2_b64,
+                // which the LDS serves at half the rate (8 cycles per KB against 4 for two
+                // ds_read_b64, MI355X_MICROARCH.md LDS table).  Issued as inline assembly, then
+                // one lgkmcnt(0) that all 16 values pass through (so no use moves above it).
+                const uint32_t la = lds_addr(rb + pad(t));
+                R u[G::E];
+                static_for<0, G::E>([&](auto M) {
+                    constexpr int C = M * G::TPS;
+                    constexpr int off = 8 * (C + (C >> 4));  // pad_plus<C>(0), C = 0 mod 16
+                    ds_read_b64_at<off>(u[M], la);
+                });
+                lgkm_wait16(u);
+                static_for<0, G::E>([&](auto M) {
+                    if (im) x[M].im = u[M]; else x[M].re = u[M];
+                });
+            } else if constexpr (G::TPS % 16 == 0) {
                 const int pt = pad(t);
                 static_for<0, G::E>([&](auto M) {
                     const R u = rb[pad_plus<M * G::TPS>(pt)];
@@ -918,26 +982,38 @@ __host__ __device__ inline double fx_value(unsigned long long l0, unsigned long 
 // offsets of the eight entries still fit the per-element code bytes), the same decisions and
 // bit handling as adaptive_diff; both FMAs of each axis in asm (the clamp bit, and no in-place
 // v_fmac rebuilding the rounding constant).
-struct OrderParams64 {
-    double mul, add, smax;  // level coordinate / (side - 1) = z mul - add, clamped; times smax
-    uint32_t meta, pad;
+// Two 16-byte vectors, each read by one ds_read_b128: ma = {mul, add}: level coordinate / (side - 1)
+// = z mul - add, clamped; times smax; sm = {smax, meta} with the meta word in the low half of the
+// second element's bits (written and read through bit casts, never as arithmetic).  Field by field
+// the compiler read ds_read2_b64 + ds_read_b64 + ds_read_b32 per element, and the 2-address read
+// serves a lane group at half the rate and conflicts for entries 4 apart.
+struct alignas(16) OrderParams64 {
+    f64x2 ma, sm;
+    __device__ static OrderParams64 make(double mul, double add, double smax, uint32_t meta) {
+        return OrderParams64{f64x2{mul, add}, f64x2{smax, __builtin_bit_cast(double, (uint64_t)meta)}};
+    }
 };
+static_assert(sizeof(OrderParams64) == 32, "two 16-byte halves");
 template <bool SMALL>
 __device__ __forceinline__ uint32_t adaptive_diff64(const cpx<double> (&z)[4], const OrderParams64* const (&op)[4],
                                                     uint32_t txw, double magic) {
     uint32_t li[4], lq[4], meta[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const OrderParams64& o = *op[j];
+        const f64x2 ma = op[j]->ma;  // {mul, add}
+        const f64x2 sm = op[j]->sm;  // {smax, meta}
         double vi, vq, fi, fq;
-        asm("v_fma_f64 %0, %1, %2, -%3 clamp" : "=v"(vi) : "v"(z[j].re), "v"(o.mul), "v"(o.add));
-        asm("v_fma_f64 %0, -%1, %2, -%3 clamp" : "=v"(vq) : "v"(z[j].im), "v"(o.mul), "v"(o.add));
-        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fi) : "v"(vi), "v"(o.smax), "s"(magic));
-        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fq) : "v"(vq), "v"(o.smax), "s"(magic));
+        asm("v_fma_f64 %0, %1, %2, -%3 clamp" : "=v"(vi) : "v"(z[j].re), "v"(ma.x), "v"(ma.y));
+        asm("v_fma_f64 %0, -%1, %2, -%3 clamp" : "=v"(vq) : "v"(z[j].im), "v"(ma.x), "v"(ma.y));
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fi) : "v"(vi), "v"(sm.x), "s"(magic));
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fq) : "v"(vq), "v"(sm.x), "s"(magic));
         li[j] = (uint32_t)__builtin_bit_cast(uint64_t, fi);
         lq[j] = (uint32_t)__builtin_bit_cast(uint64_t, fq);
         asm("" : "+v"(li[j]), "+v"(lq[j]));
-        meta[j] = o.meta;
+        // (the meta word through a bit cast of the whole vector: clang 20 resolved a bit cast of the
+        // element sm.y to element 0's register)
+        typedef uint32_t u32x4m __attribute__((ext_vector_type(4)));
+        meta[j] = __builtin_bit_cast(u32x4m, sm).z;
     }
     return adaptive_combine<SMALL>(li, lq, meta, txw);
 }

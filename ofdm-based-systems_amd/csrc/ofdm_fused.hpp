@@ -736,6 +736,8 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                     static_assert(LT <= kWinTaps, "window FIR taps");
                     constexpr int WH = 8 + LT - 1;
                     C* crow = (C*)row;
+                    // (a complex sample as one ds_write_b128: as two ds_write_b64 -- 12 LDS cycles per KB
+                    // against 13 -- TX e ran 4.78 -> 5.02 ms, profiles/r04m_ab_fir_write_b64.txt)
                     auto st16 = [&](int slot_, C v) { *(f64x2*)(crow + slot_) = f64x2{v.re, v.im}; };
                     auto ld16 = [&](const C* p) { const f64x2 u = *(const f64x2*)p; return mk<R>(u.x, u.y); };
                     const bool live = active && c >= 0;
@@ -1125,14 +1127,13 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     if constexpr (FB == 1 && sizeof(R) == 8) {
         if (threadIdx.x < 8) {
-            OrderParams64 o{0.0, 0.0, 0.0, 0u, 0u};  // unused subcarrier: level 0, no bits
+            OrderParams64 o = OrderParams64::make(0.0, 0.0, 0.0, 0u);  // unused subcarrier: level 0, no bits
             if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
                 const AxisInfo ax = cm.axis[threadIdx.x];
                 const double span = (double)(ax.side - 1);
-                o.mul = ax.inv_step * cm.scale / span;  // the FFT output stays unscaled
-                o.add = ax.lev0 * ax.inv_step / span;   // negated in the FMA
-                o.smax = span;
-                o.meta = ((1u << ax.bits) - 1u) | ((1u << ax.hbits) << 8);
+                o = OrderParams64::make(ax.inv_step * cm.scale / span,  // mul: the FFT output stays unscaled
+                                        ax.lev0 * ax.inv_step / span,   // add: negated in the FMA
+                                        span, ((1u << ax.bits) - 1u) | ((1u << ax.hbits) << 8));
             }
             ordt[threadIdx.x] = o;
         }

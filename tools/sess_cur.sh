@@ -1,9 +1,10 @@
 #!/bin/bash
-# steady-state traces + PMC of the final build (30 timed steps after the bench's clock ramp)
 set -o pipefail
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-for c in b c d e; do
-  PROF_STEPS=30 bash tools/profile.sh r04j_${c}_f64 --config $c --precision f64 --warmup 2 --ramp-seconds 0.25 > gpurun_out/r04j_prof_$c.txt 2>&1
-  rc=$?; echo "$c rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/r04j_prof_$c.txt; exit $rc; }
-  grep -h "k_tx\|k_rx" gpurun_out/prof_r04j_${c}_f64/trace/*kernel_stats.csv | cut -c1-120
-done
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/r04m_gpu_tests.txt 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/r04m_gpu_tests.txt; [ $rc -eq 0 ] || exit $rc
+AB_REPS=2 AB_STEPS=100 AB_ARGS="--precision f64 --no-variant" bash tools/ab.sh "default fw64" "b c d e" > gpurun_out/r04m_ab.txt 2>&1
+rc=$?; echo "ab rc=$rc"; cat gpurun_out/r04m_ab.txt
+for v in default fw64; do for c in b c d e; do python -c "import json; d=json.load(open('gpurun_out/ab_${v}_${c}_1.json')); print('$v','$c', d.get('ber'))"; done; done
+exit $rc
