@@ -487,6 +487,9 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
 #ifndef OFDM_SPLIT_WRITE_B64
 #define OFDM_SPLIT_WRITE_B64 1
 #endif
+#ifndef OFDM_SPLIT_XL
+#define OFDM_SPLIT_XL 1
+#endif
 // 32-bit LDS address of a pointer into __shared__ memory
 template <typename T>
 __device__ __forceinline__ uint32_t lds_addr(const T* p) {
@@ -563,12 +566,26 @@ __device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb,
 #pragma unroll
             for (int r = 0; r < RAD; ++r) x[q + r * NB] = v[q][r];
     } else {
+        // Exchange layouts of the radix-16 passes at TPS >= 64 (N >= 1024), for the single 8-byte
+        // accesses (ds_write_b64: 16-lane groups over 32 banks; ds_read_b64: 32-lane groups over
+        // 64): after pass 1, element e = 16 t + r at (TPS + 2) r + t; after pass 2, at e itself.
+        // Both are conflict-free for the writes (lane t, fixed r) and the reads (e = t + TPS m);
+        // pad() costs the reads one conflict per 32 lanes (128 cycles per N = 1024 symbol,
+        // SQ_LDS_BANK_CONFLICT 133 per symbol, profiles/r04n_counters_stall_c_f64.txt).  Rows fit: 16 TPS + 30 < PADN.
+        constexpr bool XL = sizeof(R) == 8 && OFDM_SPLIT_XL && OFDM_SPLIT_READ_B64 && OFDM_SPLIT_WRITE_B64 && G::TPS >= 64 &&
+                            RAD == 16 && NB == 1 && (LOGNS == 0 || LOGNS == 4);
         auto put = [&](bool im) {
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
                 const int j = t + q * G::TPS;
                 const int idx = ((j >> LOGNS) << (LOGNS + LOGR)) + (j & (NS - 1));
-                if constexpr (sizeof(R) == 8 && OFDM_SPLIT_WRITE_B64 && (NS % 16 == 0 || NS == 1)) {
+                if constexpr (XL) {
+                    const uint32_t la = lds_addr(rb + (LOGNS == 0 ? t : idx));
+                    static_for<0, RAD>([&](auto Rr) {
+                        constexpr int off = 8 * (LOGNS == 0 ? (G::TPS + 2) * Rr : 16 * Rr);
+                        ds_write_b64_at<off>(la, im ? v[q][Rr].im : v[q][Rr].re);
+                    });
+                } else if constexpr (sizeof(R) == 8 && OFDM_SPLIT_WRITE_B64 && (NS % 16 == 0 || NS == 1)) {
                     // one ds_write_b64 per element (the compiler's ds_write2_b64 pairs cost 13 LDS
                     // cycles per KB against 12 for two single writes); NS = 1: idx = 0 mod 16, so
                     // pad(idx + r) = pad(idx) + r
@@ -593,11 +610,13 @@ __device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb,
                 // which the LDS serves at half the rate (8 cycles per KB against 4 for two
                 // ds_read_b64, MI355X_MICROARCH.md LDS table).  Issued as inline assembly, then
                 // one lgkmcnt(0) that all 16 values pass through (so no use moves above it).
-                const uint32_t la = lds_addr(rb + pad(t));
+                const uint32_t la =
+                    lds_addr(rb + (!XL ? pad(t) : LOGNS == 0 ? (G::TPS + 2) * (t & 15) + (t >> 4) : t));
                 R u[G::E];
                 static_for<0, G::E>([&](auto M) {
                     constexpr int C = M * G::TPS;
-                    constexpr int off = 8 * (C + (C >> 4));  // pad_plus<C>(0), C = 0 mod 16
+                    constexpr int off = 8 * (!XL ? C + (C >> 4)  // pad_plus<C>(0), C = 0 mod 16
+                                             : LOGNS == 0 ? C / 16 : C);
                     ds_read_b64_at<off>(u[M], la);
                 });
                 lgkm_wait16(u);
