@@ -188,6 +188,12 @@ constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && L
 #ifndef OFDM_F64_FIR_WAVES
 #define OFDM_F64_FIR_WAVES 2
 #endif
+// N = 4096 (config e, 4 waves per symbol): 3 waves per SIMD (168 VGPRs, 18 dwords spilled) --
+// TX e 4.65 -> 4.46 ms, 2.833 -> 2.877e7 symbols/s (profiles/r04q_ab_e_fir_3waves.txt); at N = 1024 /
+// 2048 the same step spills 39 / 51 dwords (config c measured 15 % slower, profiles/r04b_ab_fir.txt)
+#ifndef OFDM_F64_FIR_WAVES_4K
+#define OFDM_F64_FIR_WAVES_4K 3
+#endif
 // complex64 throughput kernels at N >= 2048 (configs d, e): workgroup and waves per SIMD of RX
 // and of the window-FIR TX (two or four waves per symbol).  With the compact twiddle tables the
 // LDS no longer caps a CU at two workgroups, so 3 waves per SIMD fit: config e RX 3.37 -> 2.84 ms
@@ -239,7 +245,7 @@ constexpr int tx_block() {
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
 template <typename R, int FB, int LOGN, int LT>
 constexpr int tx_waves() {
-    if (sizeof(R) == 8 && FB > 0) return LT == 0 ? OFDM_F64_TX_WAVES : OFDM_F64_FIR_WAVES;
+    if (sizeof(R) == 8 && FB > 0) return LT == 0 ? OFDM_F64_TX_WAVES : (LOGN >= 12 ? OFDM_F64_FIR_WAVES_4K : OFDM_F64_FIR_WAVES);
     if (FB > 0 && LT > 0 && LOGN > 10) return OFDM_TX_BIG_WFIR_WAVES;
     return block_waves(tx_block<R, FB, LOGN, LT>(), FB > 0 && LT > 0 ? OFDM_TX_WFIR_WAVES : OFDM_TX_WAVES);
 }
