@@ -79,7 +79,7 @@ def test_sweep_grid_and_crossing():
 
 
 def test_bench_sweep_two_ranks():
-    """`bench.py --sweep --gpus 2`: one step = every point of the sweep, sharded over the ranks,
+    """`bench.py --sweep --gpus 2` (config (c) by default): one step = every point of the sweep, sharded over the ranks,
     pipelined through run_pipelined (one SNR per run); the line carries the per-point BER."""
     import subprocess
     import sys
@@ -89,13 +89,15 @@ def test_bench_sweep_two_ranks():
                                          os.path.join(ROOT, "ofdm-based-systems_amd"), env.get("PYTHONPATH", "")])
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                        "--engine-factory", "bench_double:make_engine", "--config", "c", "--sweep", "--symbols", "1",
+                        "--engine-factory", "bench_double:make_engine", "--sweep", "--symbols", "1",
                         "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-ber-check"],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["config"]["symbols_per_step"] == 80
+    # --sweep without --config measures the sweep BASELINE configs[2] names: config (c)
+    assert d["config"]["workload"].startswith("config (c)"), d["config"]["workload"]
     sw = d["sweep"]
     assert sw["points"] == 40 and len(sw["ber"]) == 40 and sw["snr_db"] == bench.SWEEP_GRID
     assert sw["ber"][0] > sw["ber"][-1]  # 0 dB vs 30 dB
