@@ -401,6 +401,43 @@ __device__ __forceinline__ void sym_sync() {
     }
 }
 
+// OFDM_SPLIT_READ_B64: the split exchange's reads as single ds_read_b64 (inline assembly) instead of
+// the compiler's ds_read2_b64 pairs
+#ifndef OFDM_SPLIT_READ_B64
+#define OFDM_SPLIT_READ_B64 1
+#endif
+// OFDM_SPLIT_WRITE_B64: the exchange's writes as single ds_write_b64 (inline assembly) instead of the
+// compiler's ds_write2_b64 pairs (c 1.196 -> 1.218e8, d 5.43 -> 5.51e7 symbols/s,
+// profiles/r04l_ab_orderparams_writeb64.txt)
+#ifndef OFDM_SPLIT_WRITE_B64
+#define OFDM_SPLIT_WRITE_B64 1
+#endif
+#ifndef OFDM_SPLIT_XL
+#define OFDM_SPLIT_XL 1
+#endif
+// 32-bit LDS address of a pointer into __shared__ memory
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(const T* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) T*)p;
+}
+// one ds_read_b64 at LDS byte address la + OFF (inline assembly: no lgkmcnt accounting by the compiler)
+template <int OFF>
+__device__ __forceinline__ void ds_read_b64_at(double& d, uint32_t la) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(d) : "v"(la), "i"(OFF) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void ds_write_b64_at(uint32_t la, double d) {
+    asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(la), "v"(d), "i"(OFF) : "memory");
+}
+// s_waitcnt lgkmcnt(0) that the 16 values read by inline-assembly LDS loads pass through
+__device__ __forceinline__ void lgkm_wait16(double (&u)[16]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
+                   "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
+                 :
+                 : "memory");
+}
+
 // One Stockham pass with the data distribution "thread t owns elements t + i*TPS".
 // FIRST: inputs come from x[] (valid because the first pass has RAD = E, STRIDE = TPS);
 // LAST: outputs stay in x[] (the last pass writes j + r*NS with j = t + q*TPS and
@@ -414,10 +451,31 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
     constexpr int NB = G::E / RAD;
     constexpr int STRIDE = G::N / RAD;
     cpx<R> v[NB][RAD];
+    // complex64 rows at N = 1024..4096 (8-byte elements): the exchanges as single ds_read_b64 /
+    // ds_write_b64 in the conflict-free layouts of the split complex128 exchange (reg_pass_split):
+    // after pass 1 element e = 16 t + r at (TPS + 2) r + t, after pass 2 at e
+    constexpr bool XLC = sizeof(cpx<R>) == 8 && OFDM_SPLIT_XL && OFDM_SPLIT_READ_B64 && OFDM_SPLIT_WRITE_B64 &&
+                         LOGN >= 10 && LOGN <= 12 && G::E == 16 && (LOGNS == 0 || LOGNS == 4 || LOGNS == 8);
     if constexpr (FIRST) {
         static_assert(NB == 1 && STRIDE == G::TPS, "first pass consumes the register layout");
 #pragma unroll
         for (int r = 0; r < RAD; ++r) v[0][r] = x[r];
+    } else if constexpr (XLC) {
+        static_assert(NB * RAD == 16, "one read per element");
+        const uint32_t la = lds_addr(buf + (LOGNS == 4 ? (G::TPS + 2) * (t & 15) + (t >> 4) : t));
+        double u[16];
+        static_for<0, NB>([&](auto Q) {
+            static_for<0, RAD>([&](auto Rr) {
+                constexpr int off = 8 * (LOGNS == 4 ? (G::TPS / 16) * Rr : Q * G::TPS + Rr * STRIDE);
+                ds_read_b64_at<off>(u[Q * RAD + Rr], la);
+            });
+        });
+        lgkm_wait16(u);
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+#pragma unroll
+            for (int r = 0; r < RAD; ++r) v[q][r] = __builtin_bit_cast(cpx<R>, u[q * RAD + r]);
+        if constexpr (!LAST) sym_sync<G::TPS>();  // every read done before the rewrite
     } else if constexpr (G::TPS % 16 == 0 && STRIDE % 16 == 0) {
         const int pt = pad(t);  // every read is pad(t) + a constant
         static_for<0, NB>([&](auto Q) {
@@ -464,6 +522,13 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
         if constexpr (LAST) {
 #pragma unroll
             for (int r = 0; r < RAD; ++r) x[q + r * NB] = v[q][r];
+        } else if constexpr (XLC) {
+            const int idx = ((j >> LOGNS) << (LOGNS + LOGR)) + k;
+            const uint32_t la = lds_addr(buf + (LOGNS == 0 ? j : idx));
+            static_for<0, RAD>([&](auto Rr) {
+                constexpr int off = 8 * (LOGNS == 0 ? (G::TPS + 2) * Rr : 16 * Rr);
+                ds_write_b64_at<off>(la, __builtin_bit_cast(double, v[q][Rr]));
+            });
         } else if constexpr (NS % 16 == 0) {
             const int pi = pad(((j >> LOGNS) << (LOGNS + LOGR)) + k);
             static_for<0, RAD>([&](auto Rr) { buf[pad_plus<Rr * NS>(pi)] = v[q][Rr]; });
@@ -474,43 +539,6 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
         }
     }
     if constexpr (!LAST) sym_sync<G::TPS>();
-}
-
-// OFDM_SPLIT_READ_B64: the split exchange's reads as single ds_read_b64 (inline assembly) instead of
-// the compiler's ds_read2_b64 pairs
-#ifndef OFDM_SPLIT_READ_B64
-#define OFDM_SPLIT_READ_B64 1
-#endif
-// OFDM_SPLIT_WRITE_B64: the exchange's writes as single ds_write_b64 (inline assembly) instead of the
-// compiler's ds_write2_b64 pairs (c 1.196 -> 1.218e8, d 5.43 -> 5.51e7 symbols/s,
-// profiles/r04l_ab_orderparams_writeb64.txt)
-#ifndef OFDM_SPLIT_WRITE_B64
-#define OFDM_SPLIT_WRITE_B64 1
-#endif
-#ifndef OFDM_SPLIT_XL
-#define OFDM_SPLIT_XL 1
-#endif
-// 32-bit LDS address of a pointer into __shared__ memory
-template <typename T>
-__device__ __forceinline__ uint32_t lds_addr(const T* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) T*)p;
-}
-// one ds_read_b64 at LDS byte address la + OFF (inline assembly: no lgkmcnt accounting by the compiler)
-template <int OFF>
-__device__ __forceinline__ void ds_read_b64_at(double& d, uint32_t la) {
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(d) : "v"(la), "i"(OFF) : "memory");
-}
-template <int OFF>
-__device__ __forceinline__ void ds_write_b64_at(uint32_t la, double d) {
-    asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(la), "v"(d), "i"(OFF) : "memory");
-}
-// s_waitcnt lgkmcnt(0) that the 16 values read by inline-assembly LDS loads pass through
-__device__ __forceinline__ void lgkm_wait16(double (&u)[16]) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
-                   "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
-                 :
-                 : "memory");
 }
 
 // complex128 throughput kernels: the transposes between passes go through a row of N doubles,
