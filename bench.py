@@ -279,7 +279,7 @@ class Runtime:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
         self.cpu = cpu
-        self.group = None
+        self.group = self.host_group = None
         # OFDM_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a 1-GPU box
         # (with --backend gloo; RCCL refuses two ranks on one GPU)
         self.dev = int(os.environ.get("OFDM_BENCH_DEVICE", self.local))
@@ -294,6 +294,9 @@ class Runtime:
                 dist.init_process_group(backend)
             self.group = dist.group.WORLD
             self.world = dist.get_world_size()
+            # host-side group for the closing barrier: while rank 0 times the CPU baseline, the other
+            # ranks wait on a socket (gloo) instead of a device collective whose host thread spins
+            self.host_group = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else self.group
 
     def sync(self):
         if not self.cpu:
@@ -327,7 +330,7 @@ class Runtime:
         if self.world > 1:
             import torch.distributed as dist
 
-            dist.barrier()
+            dist.barrier(group=self.host_group)
             dist.destroy_process_group()
 
 
@@ -580,7 +583,9 @@ def main():
         eng64 = make_engine(cfg, "f64")
         out["ber_vs_reference"] = ber_vs_reference(eng64, N, engine.cp, snr, head["ber"], head["bits"],
                                                    symbols=max(2000, 16000 * 1024 // N))
-    if rt.rank == 0 and rt.world == 1 and not args.no_cpu_baseline:
+    if rt.rank == 0 and not args.no_cpu_baseline:
+        # on rank 0 after every GPU measurement, for any number of ranks (the other ranks wait at
+        # rt.finish()): the reference CPU path on the node's host cores, in the same run
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
     if rt.rank == 0:
         print(json.dumps(out), flush=True)
@@ -628,7 +633,7 @@ def sweep_main(rt: Runtime, args, cfg, factory):
         out["ber_1e-4_crossing_db"]["reference_ber"] = dict(zip(near, ref))
         out["delta_db_at_1e-4"] = None if c_phx is None or c_ref is None else c_phx - c_ref
         out["bar_db"] = 0.05
-    if rt.rank == 0 and rt.world == 1 and not args.no_cpu_baseline:
+    if rt.rank == 0 and not args.no_cpu_baseline:
         cpu_cfg = (N, M, ch, ratio, eq_name, 27.75, desc)
         out["cpu_baseline"] = cpu_baseline(cpu_cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
         out["cpu_baseline"]["sample"] += " (at the sweep's 27.75 dB point: the CPU cost does not depend on the SNR)"

@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 namespace ofdm {
 
@@ -420,22 +421,45 @@ template <typename T>
 __device__ __forceinline__ uint32_t lds_addr(const T* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) T*)p;
 }
-// one ds_read_b64 at LDS byte address la + OFF (inline assembly: no lgkmcnt accounting by the compiler)
-template <int OFF>
-__device__ __forceinline__ void ds_read_b64_at(double& d, uint32_t la) {
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(d) : "v"(la), "i"(OFF) : "memory");
-}
 template <int OFF>
 __device__ __forceinline__ void ds_write_b64_at(uint32_t la, double d) {
     asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(la), "v"(d), "i"(OFF) : "memory");
 }
-// s_waitcnt lgkmcnt(0) that the 16 values read by inline-assembly LDS loads pass through
-__device__ __forceinline__ void lgkm_wait16(double (&u)[16]) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
-                   "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
-                 :
-                 : "memory");
+// 16 ds_read_b64 at LDS byte addresses la + O_m and their s_waitcnt lgkmcnt(0) as ONE inline-assembly
+// statement: the compiler's wait-count pass does not track inline-assembly LDS loads, so with the
+// reads and the wait in separate statements nothing would stop it from copying (or spilling) a
+// destination register between a read and the wait -- a stale value without any error.  Inside
+// one statement no instruction can be placed between them; the destinations are early-clobber, so
+// none of them shares a register with the address.
+template <int... O>
+__device__ __forceinline__ void ds_read16_b64(double (&u)[16], uint32_t la) {
+    static_assert(sizeof...(O) == 16, "16 offsets");
+    constexpr int o[16] = {O...};
+    asm volatile(
+        "ds_read_b64 %0, %16 offset:%17\n\tds_read_b64 %1, %16 offset:%18\n\t"
+        "ds_read_b64 %2, %16 offset:%19\n\tds_read_b64 %3, %16 offset:%20\n\t"
+        "ds_read_b64 %4, %16 offset:%21\n\tds_read_b64 %5, %16 offset:%22\n\t"
+        "ds_read_b64 %6, %16 offset:%23\n\tds_read_b64 %7, %16 offset:%24\n\t"
+        "ds_read_b64 %8, %16 offset:%25\n\tds_read_b64 %9, %16 offset:%26\n\t"
+        "ds_read_b64 %10, %16 offset:%27\n\tds_read_b64 %11, %16 offset:%28\n\t"
+        "ds_read_b64 %12, %16 offset:%29\n\tds_read_b64 %13, %16 offset:%30\n\t"
+        "ds_read_b64 %14, %16 offset:%31\n\tds_read_b64 %15, %16 offset:%32\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(u[0]), "=&v"(u[1]), "=&v"(u[2]), "=&v"(u[3]), "=&v"(u[4]), "=&v"(u[5]), "=&v"(u[6]), "=&v"(u[7]),
+          "=&v"(u[8]), "=&v"(u[9]), "=&v"(u[10]), "=&v"(u[11]), "=&v"(u[12]), "=&v"(u[13]), "=&v"(u[14]),
+          "=&v"(u[15])
+        : "v"(la), "i"(o[0]), "i"(o[1]), "i"(o[2]), "i"(o[3]), "i"(o[4]), "i"(o[5]), "i"(o[6]), "i"(o[7]),
+          "i"(o[8]), "i"(o[9]), "i"(o[10]), "i"(o[11]), "i"(o[12]), "i"(o[13]), "i"(o[14]), "i"(o[15])
+        : "memory");
+}
+// the same with byte offsets Off::at(m), m = 0..15 (Off: a class with a static constexpr at(int))
+template <class Off, int... M>
+__device__ __forceinline__ void ds_read16_b64_seq(double (&u)[16], uint32_t la, std::integer_sequence<int, M...>) {
+    ds_read16_b64<Off::at(M)...>(u, la);
+}
+template <class Off>
+__device__ __forceinline__ void ds_read16_b64(double (&u)[16], uint32_t la) {
+    ds_read16_b64_seq<Off>(u, la, std::make_integer_sequence<int, 16>{});
 }
 
 // One Stockham pass with the data distribution "thread t owns elements t + i*TPS".
@@ -464,13 +488,12 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
         static_assert(NB * RAD == 16, "one read per element");
         const uint32_t la = lds_addr(buf + (LOGNS == 4 ? (G::TPS + 2) * (t & 15) + (t >> 4) : t));
         double u[16];
-        static_for<0, NB>([&](auto Q) {
-            static_for<0, RAD>([&](auto Rr) {
-                constexpr int off = 8 * (LOGNS == 4 ? (G::TPS / 16) * Rr : Q * G::TPS + Rr * STRIDE);
-                ds_read_b64_at<off>(u[Q * RAD + Rr], la);
-            });
-        });
-        lgkm_wait16(u);
+        struct Off {  // element u[Q RAD + Rr]
+            static constexpr int at(int m) {
+                return 8 * (LOGNS == 4 ? (G::TPS / 16) * (m % RAD) : (m / RAD) * G::TPS + (m % RAD) * STRIDE);
+            }
+        };
+        ds_read16_b64<Off>(u, la);
 #pragma unroll
         for (int q = 0; q < NB; ++q)
 #pragma unroll
@@ -523,6 +546,8 @@ __device__ __forceinline__ void reg_pass(cpx<R> (&x)[Geo<LOGN>::E], cpx<R>* buf,
 #pragma unroll
             for (int r = 0; r < RAD; ++r) x[q + r * NB] = v[q][r];
         } else if constexpr (XLC) {
+            // the per-radix offset 16 Rr below assumes NS = 16 whenever LOGNS != 0
+            static_assert(LOGNS == 0 || (LOGNS == 4 && RAD == 16 && NB == 1), "XLC write layout");
             const int idx = ((j >> LOGNS) << (LOGNS + LOGR)) + k;
             const uint32_t la = lds_addr(buf + (LOGNS == 0 ? j : idx));
             static_for<0, RAD>([&](auto Rr) {
@@ -636,18 +661,19 @@ __device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb,
             if constexpr (G::TPS % 16 == 0 && sizeof(R) == 8 && OFDM_SPLIT_READ_B64) {
                 // one ds_read_b64 per element: the compiler pairs the reads into ds_read2_b64,
                 // which the LDS serves at half the rate (8 cycles per KB against 4 for two
-                // ds_read_b64, MI355X_MICROARCH.md LDS table).  Issued as inline assembly, then
-                // one lgkmcnt(0) that all 16 values pass through (so no use moves above it).
+                // ds_read_b64, MI355X_MICROARCH.md LDS table).  Issued with their lgkmcnt(0) as one
+                // inline-assembly statement (ds_read16_b64).
                 const uint32_t la =
                     lds_addr(rb + (!XL ? pad(t) : LOGNS == 0 ? (G::TPS + 2) * (t & 15) + (t >> 4) : t));
+                static_assert(G::E == 16, "16 elements per lane");
                 R u[G::E];
-                static_for<0, G::E>([&](auto M) {
-                    constexpr int C = M * G::TPS;
-                    constexpr int off = 8 * (!XL ? C + (C >> 4)  // pad_plus<C>(0), C = 0 mod 16
-                                             : LOGNS == 0 ? C / 16 : C);
-                    ds_read_b64_at<off>(u[M], la);
-                });
-                lgkm_wait16(u);
+                struct Off {
+                    static constexpr int at(int m) {
+                        return 8 * (!XL ? m * G::TPS + ((m * G::TPS) >> 4)  // pad_plus<C>(0), C = 0 mod 16
+                                        : LOGNS == 0 ? m * G::TPS / 16 : m * G::TPS);
+                    }
+                };
+                ds_read16_b64<Off>(u, la);
                 static_for<0, G::E>([&](auto M) {
                     if (im) x[M].im = u[M]; else x[M].re = u[M];
                 });

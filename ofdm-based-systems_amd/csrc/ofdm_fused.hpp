@@ -135,12 +135,10 @@ __device__ __forceinline__ T buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t voff,
     static_assert(sizeof(T) == 16, "16-byte element");
     return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, NT ? 2 : 0));
 }
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-template <typename T, bool NT = false>
-__device__ __forceinline__ void buf_store16(T v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-    static_assert(sizeof(T) == 16, "16-byte element");
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, (int)voff, (int)soff, NT ? 2 : 0);
-}
+// (No buffer-store counterpart, deliberately: buffer_store_dwordx4 with a register SGPR offset
+// corrupted the low data dword on gfx950 -- the compiler inserts no wait state between such a store
+// and the next VALU write of its data VGPRs, DESIGN.md section 4.  Stores use the global_store forms;
+// tests/test_isa_guard.py rejects any buffer store in the fused kernels' code.)
 
 // complex128 multipath TX of square QAM (the plan sends only separable LUTs to the throughput
 // kernels): map through the two axis tables instead of the complex LUT (TX c 5.13 -> 5.12, e 5.26
@@ -271,6 +269,10 @@ __host__ __device__ constexpr int wfir_out(int kk) { return (kk & ~7) | ((kk ^ (
 #ifndef OFDM_F64_RX_SOLO_WAVES
 #define OFDM_F64_RX_SOLO_WAVES 3
 #endif
+// the complex128 adaptive receiver at N = 2048 (config d): one 128-thread symbol per workgroup
+#ifndef OFDM_F64_RX_ADAPT_WAVES
+#define OFDM_F64_RX_ADAPT_WAVES 2
+#endif
 // the OFDM_F64_RX_BLOCK / _WAVES shape: no-equaliser RX of 64/256-QAM at N = 1024 (at 128 VGPRs the
 // QPSK / 16-QAM and smaller-N kernels spill 22-33 dwords, so they stay at 768 threads, 3 waves;
 // with an equaliser the 16 KB coefficient table beside 16 symbols' rows exceeds the LDS)
@@ -296,7 +298,7 @@ constexpr int rx_block() {
 }
 template <typename R, int FB, int LOGN, int EQ, bool MV = false>
 constexpr int rx_waves() {
-    if (f64_rx_solo<R, FB, LOGN>()) return (FB == 1 || MV) ? 2 : OFDM_F64_RX_SOLO_WAVES;
+    if (f64_rx_solo<R, FB, LOGN>()) return FB == 1 ? OFDM_F64_RX_ADAPT_WAVES : MV ? 2 : OFDM_F64_RX_SOLO_WAVES;
     if (sizeof(R) == 8 && FB > 0)
         return (LOGN > 10 || FB == 1) ? 2 : (f64_rx_wide<FB, LOGN, EQ, MV>() ? OFDM_F64_RX_WAVES : 3);
     if (FB > 0 && LOGN > 10) return OFDM_RX_BIG_WAVES;

@@ -6,6 +6,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 from conftest import ROOT
 
 import bench
@@ -45,9 +46,12 @@ def test_adaptive_config_orders_follow_the_reference_rule():
     assert 0 < bps < 8 * N and all(o == 0 or (o & (o - 1)) == 0 for o in orders)
 
 
-def test_bench_gpus_flag_launches_ranks():
-    """`bench.py --gpus 2` (no torch.distributed environment) launches two ranks itself and
-    reports n_gpus 2 from the process group (gloo, CPU engine double instead of the kernels)."""
+@pytest.mark.parametrize("gpus", [2, 4])
+def test_bench_gpus_flag_launches_ranks(gpus):
+    """`bench.py --gpus N` (no torch.distributed environment) launches N ranks itself and
+    reports n_gpus N from the process group (gloo, CPU engine double instead of the kernels); the
+    line carries the CPU baseline beside the N-rank measurement (north star: 1/2/4/8 GPUs alongside
+    the reference CPU path timed on the node's own host cores, in the same run)."""
     import subprocess
     import sys
 
@@ -55,18 +59,20 @@ def test_bench_gpus_flag_launches_ranks():
     env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
                                          os.path.join(ROOT, "ofdm-based-systems_amd"), env.get("PYTHONPATH", "")])
     env.pop("WORLD_SIZE", None)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo",
                         "--engine-factory", "bench_double:make_engine", "--config", "b", "--symbols", "3",
-                        "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-ber-check", "--no-variant",
+                        "--steps", "2", "--warmup", "1", "--cpu-sample", "2", "--no-ber-check", "--no-variant",
                         "--ramp-seconds", "0"],
-                       env=env, capture_output=True, text=True, timeout=300)
+                       env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1, r.stdout
     d = json.loads(line[0])
-    assert d["n_gpus"] == 2 and d["devices"] == ["cpu", "cpu"]
-    assert d["config"]["symbols_per_step"] == 6 and d["scaling"] == "weak"
+    assert d["n_gpus"] == gpus and d["devices"] == ["cpu"] * gpus
+    assert d["config"]["symbols_per_step"] == 3 * gpus and d["scaling"] == "weak"
     assert d["steps"] == 2 and d["warmup"] == 1 and d["value"] > 0
+    cb = d["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["unit"] == "OFDM symbols/s"
 
 
 def test_sweep_grid_and_crossing():

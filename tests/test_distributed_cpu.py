@@ -118,10 +118,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, batch, out):
+def _worker(rank, world, port, batch, S, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    c = CASE
+    c = dict(CASE, S=S)
     h = channel(c["ch"])
     cp = len(h) - 1
     b = int(np.log2(c["M"]))
@@ -133,9 +133,11 @@ def _worker(rank, world, port, batch, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,batch", [(2, None), (2, 5), (3, None)])
-def test_sharded_engine_matches_single_process_oracle(world, batch):
-    c = CASE
+@pytest.mark.parametrize("world,batch,S", [(2, None, 48), (2, 5, 48), (3, None, 48),
+                                           (4, None, 50), (4, 5, 50), (8, None, 53), (8, 3, 53)])
+def test_sharded_engine_matches_single_process_oracle(world, batch, S):
+    """world 4 / 8 with S not divisible by the rank count (shards of unequal length, 53 = 6 x 8 + 5)"""
+    c = dict(CASE, S=S)
     h = channel(c["ch"])
     cp = len(h) - 1
     b = int(np.log2(c["M"]))
@@ -143,7 +145,7 @@ def test_sharded_engine_matches_single_process_oracle(world, batch):
     ref = O.run_fixed(tx, c["S"] * c["N"] * b, c["N"], c["M"], h, cp, c["eq"], c["snr"], nz)
     assert ref.bit_errors > 0
     out = mp.Manager().dict()
-    mp.spawn(_worker, args=(world, _free_port(), batch, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), batch, S, out), nprocs=world, join=True)
     for r in range(world):
         be, se, papr, _ = out[r]
         assert (be, se) == (ref.bit_errors, ref.symbol_errors), (r, be, se, ref)
@@ -154,20 +156,20 @@ def test_sharded_engine_matches_single_process_oracle(world, batch):
     assert {out[r][3] for r in range(world)} == {single.power_sum}
 
 
-def _pipelined_worker(rank, world, port, out):
+def _pipelined_worker(rank, world, port, S, lanes, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    c = CASE
+    c = dict(CASE, S=S)
     h = channel(c["ch"])
     eng = OracleEngine(c["N"], c["M"], h, len(h) - 1, c["eq"])
     seeds = [11, 12, 13]
     for sd in seeds:
         eng.seed_streams(sd, c["S"])
-    piped = [p.result() for p in eng.run_pipelined(c["S"], c["snr"], seeds, group=dist.group.WORLD)]
+    piped = [p.result() for p in eng.run_pipelined(c["S"], c["snr"], seeds, group=dist.group.WORLD, lanes=lanes)]
     # a y budget below two shards' buffers: the runs go through batched run_async instead
-    # (16 KB: 8 of a rank's 24 symbols per batch)
+    # (8 symbols per batch: a rank's shard spans several batches at world 2)
     small = [p.result() for p in eng.run_pipelined(c["S"], c["snr"], seeds, group=dist.group.WORLD,
-                                                   y_budget=8 * c["N"] * 16)]
+                                                   y_budget=8 * c["N"] * 16, lanes=lanes)]
     serial = [eng.run(c["S"], c["snr"], seed=sd, group=dist.group.WORLD) for sd in seeds]
     out[rank] = ([(r.bit_errors, r.symbol_errors, r.power_sum) for r in piped],
                  [(r.bit_errors, r.symbol_errors, r.power_sum) for r in serial],
@@ -175,18 +177,20 @@ def _pipelined_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_pipelined_runs_match_serial_runs():
+@pytest.mark.parametrize("world,S,lanes", [(2, 48, 1), (4, 50, 2), (8, 53, 2)])
+def test_pipelined_runs_match_serial_runs(world, S, lanes):
     """bench.py's schedule (run k+1's TX enqueued before run k's RX, asynchronous exchanges)
     gives every run the counts and statistics of LinkEngine.run with the same seed, on every
     rank, and those of the single-process oracle; so does its batched fallback when the two
-    runs' channel-sample buffers exceed y_budget."""
-    c = CASE
+    runs' channel-sample buffers exceed y_budget.  World 4 / 8 with uneven shards, and the
+    two-lane schedule of --sweep (on CPU tensors the lanes share the one host stream)."""
+    c = dict(CASE, S=S)
     h = channel(c["ch"])
     cp = len(h) - 1
     b = int(np.log2(c["M"]))
     out = mp.Manager().dict()
-    mp.spawn(_pipelined_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    for r in range(2):
+    mp.spawn(_pipelined_worker, args=(world, _free_port(), S, lanes, out), nprocs=world, join=True)
+    for r in range(world):
         piped, serial, small = out[r]
         assert piped == serial, (r, piped, serial)
         assert small == serial, (r, small, serial)
