@@ -416,6 +416,11 @@ __device__ __forceinline__ void sym_sync() {
 #ifndef OFDM_SPLIT_XL
 #define OFDM_SPLIT_XL 1
 #endif
+// OFDM_SPLIT_PERMLANE: the second exchange of the N = 1024 complex128 FFT in registers
+// (v_permlane32_swap / v_permlane16_swap, reg_pass_split) instead of through the LDS row
+#ifndef OFDM_SPLIT_PERMLANE
+#define OFDM_SPLIT_PERMLANE 1
+#endif
 // 32-bit LDS address of a pointer into __shared__ memory
 template <typename T>
 __device__ __forceinline__ uint32_t lds_addr(const T* p) {
@@ -613,11 +618,41 @@ __device__ __forceinline__ void reg_pass_split(cpx<R> (&x)[Geo<LOGN>::E], R* rb,
         }
         dft<R, RAD, INV>(v[q]);
     }
+    // N = 1024 (a symbol per wave), the exchange after the second radix-16 pass: in registers with
+    // the gfx950 cross-row swaps instead of through the LDS row.  Pass 2 leaves output r = 4 rh + rl
+    // of lane t at Stockham position 256 (t >> 4) + (t & 15) + 16 r; the last pass (radix 4) reads
+    // element t' + 64 m into x[m].  So the value moves to lane (t & 15) + 16 rl, register
+    // 4 (t >> 4) + rh: for each rh, a 4 x 4 transpose of (16-lane row t >> 4, rl), which
+    // v_permlane32_swap (rows {2,3} of one register <-> rows {0,1} of another) and
+    // v_permlane16_swap (odd rows <-> even rows) do in four swaps per 4 dwords -- 64 VALU swaps
+    // per symbol instead of 32 ds_write_b64 + 32 ds_read_b64 and their waits.
+    constexpr bool XPERM = OFDM_SPLIT_PERMLANE && sizeof(R) == 8 && G::TPS == 64 && G::E == 16 && LOGN == 10 &&
+                           LOGNS == 4 && RAD == 16 && NB == 1 && !LAST;
     if constexpr (LAST) {
 #pragma unroll
         for (int q = 0; q < NB; ++q)
 #pragma unroll
             for (int r = 0; r < RAD; ++r) x[q + r * NB] = v[q][r];
+    } else if constexpr (XPERM) {
+        typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+        static_for<0, 4>([&](auto RH) {
+            u32x4v d[4];
+#pragma unroll
+            for (int rl = 0; rl < 4; ++rl) d[rl] = __builtin_bit_cast(u32x4v, v[0][4 * RH + rl]);
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                auto s02 = __builtin_amdgcn_permlane32_swap(d[0][w], d[2][w], false, false);
+                auto s13 = __builtin_amdgcn_permlane32_swap(d[1][w], d[3][w], false, false);
+                auto s01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
+                auto s23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
+                d[0][w] = s01[0];
+                d[1][w] = s01[1];
+                d[2][w] = s23[0];
+                d[3][w] = s23[1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) x[4 * k + RH] = __builtin_bit_cast(cpx<R>, d[k]);
+        });
     } else {
         // Exchange layouts of the radix-16 passes at TPS >= 64 (N >= 1024), for the single 8-byte
         // accesses (ds_write_b64: 16-lane groups over 32 banks; ds_read_b64: 32-lane groups over

@@ -150,6 +150,11 @@ constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && L
 // VGPR, the element offsets in SGPRs) instead of four 64-bit VGPR addresses (RX b 3.09 -> 3.06,
 // c 3.75 -> 3.70 ms per step at the same occupancy, profiles/r03ab_ab.txt)
 
+// complex128 window-FIR TX: the window's LDS reads chained to the samples before them (see k_tx)
+#ifndef OFDM_FIR_STREAM
+#define OFDM_FIR_STREAM 0
+#endif
+
 // MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
 #ifndef OFDM_TX_MP_BLOCK
 #define OFDM_TX_MP_BLOCK 256
@@ -232,18 +237,48 @@ constexpr size_t tx_static_lds() {
     return lut * 2 * sizeof(R) + sep * sizeof(R);
 }
 // LT (throughput TX): 0 flat channel; 4 / 8 multipath with <= LT taps through the register
-// window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps)
-template <typename R, int FB, int LOGN, int LT>
+// window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps).  ZPW: the complex128
+// window FIR with the zero-padding guard (and its run-time flat path for a one-tap channel) compiled
+// in; without it (cyclic prefix, L > 1: the bench configs) the kernel needs ~139 VGPRs instead of
+// 205-227 and runs 3 waves per SIMD with nothing spilled (with the guard compiled in, 3 waves spilled
+// 39 / 51 dwords at N = 1024 / 2048)
+#ifndef OFDM_F64_FIR_CP3
+#define OFDM_F64_FIR_CP3 0
+#endif
+// workgroup of the 3-wave cyclic-prefix window FIR: at N = 1024 (a symbol per wave) 768 threads keep
+// one copy of the 16 KB per-pass twiddle table for 12 symbols' rows (at 256 threads the table per
+// workgroup caps a CU at two workgroups, 2 waves per SIMD); N = 2048 (two waves per symbol) 768 for
+// the adaptive tables likewise; N = 4096 one symbol per 256-thread workgroup
+#ifndef OFDM_F64_FIR3_BLOCK_10
+#define OFDM_F64_FIR3_BLOCK_10 768
+#endif
+#ifndef OFDM_F64_FIR3_BLOCK_11
+#define OFDM_F64_FIR3_BLOCK_11 768
+#endif
+template <int FB, int LOGN, int LT, bool ZPW>
+constexpr bool f64_fir_cp3() {
+    return OFDM_F64_FIR_CP3 && LT > 0 && !ZPW &&
+           f64_fir_lds(FB, LOGN, LOGN == 10 ? OFDM_F64_FIR3_BLOCK_10 : LOGN == 11 ? OFDM_F64_FIR3_BLOCK_11 : 256,
+                       true) <= 160 * 1024;
+}
+template <typename R, int FB, int LOGN, int LT, bool ZPW = false>
 constexpr int tx_block() {
-    if (sizeof(R) == 8 && FB > 0)
-        return LT == 0 ? OFDM_F64_TX_BLOCK
-                       : (f64_fir_lds(FB, LOGN, OFDM_F64_FIR_BLOCK, LT > 0) <= 160 * 1024 ? OFDM_F64_FIR_BLOCK : 256);
+    if (sizeof(R) == 8 && FB > 0) {
+        if (LT == 0) return OFDM_F64_TX_BLOCK;
+        if (f64_fir_cp3<FB, LOGN, LT, ZPW>())
+            return LOGN == 10 ? OFDM_F64_FIR3_BLOCK_10 : LOGN == 11 ? OFDM_F64_FIR3_BLOCK_11 : 256;
+        return f64_fir_lds(FB, LOGN, OFDM_F64_FIR_BLOCK, LT > 0) <= 160 * 1024 ? OFDM_F64_FIR_BLOCK : 256;
+    }
     return FB > 0 && LOGN <= 10 ? (LT != 0 ? OFDM_TX_MP_BLOCK : OFDM_TX_FAST_BLOCK) : kBlock;
 }
 constexpr int block_waves(int blk, int dflt) { return blk >= 512 ? 4 : dflt; }
-template <typename R, int FB, int LOGN, int LT>
+template <typename R, int FB, int LOGN, int LT, bool ZPW = false>
 constexpr int tx_waves() {
-    if (sizeof(R) == 8 && FB > 0) return LT == 0 ? OFDM_F64_TX_WAVES : (LOGN >= 12 ? OFDM_F64_FIR_WAVES_4K : OFDM_F64_FIR_WAVES);
+    if (sizeof(R) == 8 && FB > 0) {
+        if (LT == 0) return OFDM_F64_TX_WAVES;
+        if (f64_fir_cp3<FB, LOGN, LT, ZPW>()) return 3;
+        return LOGN >= 12 ? OFDM_F64_FIR_WAVES_4K : OFDM_F64_FIR_WAVES;
+    }
     if (FB > 0 && LT > 0 && LOGN > 10) return OFDM_TX_BIG_WFIR_WAVES;
     return block_waves(tx_block<R, FB, LOGN, LT>(), FB > 0 && LT > 0 ? OFDM_TX_WFIR_WAVES : OFDM_TX_WAVES);
 }
@@ -490,10 +525,10 @@ constexpr bool uses_tt() { return FB > 0 && fast_tt<R, LOGN>(); }
 // Each symbol group walks `chunk` consecutive OFDM symbols so the FIR tail (last L-1
 // stream samples of the previous symbol) is carried in LDS; the first symbol of a chunk
 // regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
-template <typename R, int LOGN, int FB, int LT>
-__global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOGN, LT>())) void k_tx(
+template <typename R, int LOGN, int FB, int LT, bool ZPW = false>
+__global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB, LOGN, LT, ZPW>())) void k_tx(
     TxArgs a) {
-    constexpr int BLK = tx_block<R, FB, LOGN, LT>();
+    constexpr int BLK = tx_block<R, FB, LOGN, LT, ZPW>();
     constexpr bool WFIR = FB > 0 && LT > 0;  // register window FIR
     constexpr bool TX_NT = OFDM_TX_NT || (sizeof(R) == 8 && OFDM_TX_NT_F64);  // nontemporal y stores
     using G = Geo<LOGN, BLK>;
@@ -508,7 +543,10 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
     // zero-padding guard (run-time, uniform); compiled out of the flat throughput TX (a zero
     // guard needs cp > 0, the launcher sends it to the LT = -1 kernel), where the run-time
     // row stride alone cost 15 % (config b TX 1.64 -> 1.92 ms)
-    constexpr bool ZP_OK = !(FB == 1 || (FB > 1 && LT == 0));
+    // (window FIR: only the ZPW instantiation -- the launcher sends zero padding there, and a one-tap
+    // channel without it to the flat kernel, so the CP window FIR never takes the flat path below)
+    constexpr bool ZP_OK = !(FB == 1 || (FB > 1 && LT == 0)) && (!WFIR || ZPW);
+    constexpr bool FLAT_OK = !WFIR || ZPW;
     const bool zp = ZP_OK ? (bool)cm.zpad : false;
     const int ystride = ZP_OK ? cm.ystride : N;  // stored samples per OFDM symbol: N, or N + cp (ZP)
     const int cp = cm.cp, L = LT != 0 ? a.L : 1;
@@ -677,7 +715,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                 px += pxs;
                 mx = fmax(mx, (double)mxs);
             }
-            if (L == 1) {
+            if (FLAT_OK && L == 1) {
                 // flat channel: y = h0 x, no inter-symbol memory
                 if (active && c >= 0) {
                     C* yo = yout + sl * ystride;
@@ -816,19 +854,35 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                         // every lane streams its window, live or not (under the live condition the
                         // accumulators would be conditionally defined and spill)
                         // (wfir_in(Ah + 8 t + W) = wfir_in(Ah) + 9 t + W + (W + ioff) / 8)
-                        const C* wb = crow + (wfir_in(Ah, LT) + 9 * to);
                         constexpr int IOFF = wfir_ioff(LT);
                         R T[8], U[8], V[8];
-                        // the window streamed two samples ahead of its use; the scheduling barrier
-                        // keeps the compiler from issuing all 8 + LT - 1 reads at once (a whole
-                        // window of live registers at the peak of the kernel)
+                        // the window streamed two samples ahead of its use.  Each read's LDS address
+                        // passes through an empty asm statement that takes the previous sample's
+                        // sum as an input, so the read cannot be issued before that sample arrived:
+                        // left to the compiler (even with a scheduling barrier per sample), all
+                        // 8 + LT - 1 reads were issued at once -- a whole window of 60 live VGPRs at
+                        // the register peak of the kernel
+                        typedef const __attribute__((address_space(3))) f64x2* lwin;
+                        lwin wl = (lwin)(crow + (wfir_in(Ah, LT) + 9 * to));
+                        auto ldw = [&](int k) { const f64x2 u = wl[k]; return mk<R>(u.x, u.y); };
                         C ring[3];
-                        ring[0] = ld16(wb + (IOFF >> 3));
-                        ring[1] = ld16(wb + (1 + ((1 + IOFF) >> 3)));
+                        ring[0] = ldw(IOFF >> 3);
+                        ring[1] = ldw(1 + ((1 + IOFF) >> 3));
                         static_for<0, WH>([&](auto W) {
-                            if constexpr (W + 2 < WH) ring[(W + 2) % 3] = ld16(wb + ((W + 2) + ((W + 2 + IOFF) >> 3)));
                             const C e = ring[W % 3];
                             const R sw = e.re + e.im;
+                            if constexpr (W + 2 < WH) {
+                                if constexpr (OFDM_FIR_STREAM && W > 0) {
+                                    // tied to the previous sample's accumulators (its outputs j in
+                                    // [W - LT, W - 1]): its multiply-adds are issued before this read
+                                    constexpr int j0 = W - LT < 0 ? 0 : W - LT, j1 = W - 1 > 7 ? 7 : W - 1;
+                                    auto jc = [&](int d) -> R { return T[j0 + d <= j1 ? j0 + d : j1]; };
+                                    asm volatile("" : "+v"(wl)
+                                                 : "v"(jc(0)), "v"(jc(1)), "v"(jc(2)), "v"(jc(3)), "v"(jc(4)),
+                                                   "v"(jc(5)), "v"(jc(6)), "v"(jc(7)));
+                                }
+                                ring[(W + 2) % 3] = ldw((W + 2) + ((W + 2 + IOFF) >> 3));
+                            }
                             static_for<0, LT>([&](auto Q) {  // tap Q of output j
                                 constexpr int j = W - (LT - 1) + Q;
                                 if constexpr (j >= 0 && j < 8) {
@@ -845,6 +899,15 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT>()), (tx_waves<R, FB, LOG
                             });
                             __builtin_amdgcn_sched_barrier(0);
                         });
+                        if constexpr (OFDM_FIR_STREAM) {
+                            // every accumulator final here, before the branches below (otherwise
+                            // the multiply-adds were sunk past them with the window still live)
+                            asm volatile("" : "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]),
+                                              "+v"(T[6]), "+v"(T[7]), "+v"(U[0]), "+v"(U[1]), "+v"(U[2]), "+v"(U[3]),
+                                              "+v"(U[4]), "+v"(U[5]), "+v"(U[6]), "+v"(U[7]));
+                            asm volatile("" : "+v"(V[0]), "+v"(V[1]), "+v"(V[2]), "+v"(V[3]), "+v"(V[4]), "+v"(V[5]),
+                                              "+v"(V[6]), "+v"(V[7]));
+                        }
                         if constexpr (h == 1) {
                             // zero padding: guard output N + t = sum over l > t of h_l x[N + t - l]
                             // (the guard's own samples are zero), stored and counted
@@ -1403,11 +1466,18 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                     ses += PermSlicer<8>::nonzero_bytes(d);
                     if (!all_valid) {
                         // a trailing partial byte of the run is not compared (constellation/
-                        // adaptive.py:259-263): keep the first bits (MSB first) of the valid range
+                        // adaptive.py:259-263): keep the first bits (MSB first) of the valid range.
+                        // (The table is read through an opaque pointer: otherwise the compiler
+                        // reuses the launch-invariant reads of the order codes above and keeps all
+                        // 16 entries -- or their addresses -- in registers through the symbol loop,
+                        // for a branch only the run's last symbol takes.)
+                        static_assert(sizeof(ScInfo) == 8, "ScInfo is one 8-byte word");
+                        gptr<const uint64_t> scp = (gptr<const uint64_t>)cm.sc;
+                        asm volatile("" : "+s"(scp));
                         uint32_t vm = 0;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            const ScInfo sc = cm.sc[t + (4 * q + j) * TPS];
+                            const ScInfo sc = __builtin_bit_cast(ScInfo, (uint64_t)scp[t + (4 * q + j) * TPS]);
                             if (sc.lut < 0) continue;
                             const int64_t nvb = a.n_valid_bits - (sbit + sc.bitoff);
                             const int keep = nvb <= 0 ? 0 : (nvb >= sc.bits ? sc.bits : (int)nvb);

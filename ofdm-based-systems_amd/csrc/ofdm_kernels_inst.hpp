@@ -168,9 +168,9 @@ static inline int tx_chunk(int64_t n_sym, int max_chunk, int spb, int resident) 
     return best;
 }
 
-template <typename R, int LOGN, int FB, int LT>
+template <typename R, int LOGN, int FB, int LT, bool ZPW = false>
 static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
-    constexpr int BLK = tx_block<R, FB, LOGN, LT>();
+    constexpr int BLK = tx_block<R, FB, LOGN, LT, ZPW>();
     TxArgs a = a0;
     if (FB > 0 && LT > 0) {
         if constexpr (sizeof(R) == 8) {
@@ -191,7 +191,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     if constexpr (FB > 0) {
         if (sm + tx_static_lds<R, FB, LT>() > kLdsPerCu) return tx_launch<R, LOGN, 0, -1>(a0, grid, s);
     }
-    auto fn = k_tx<R, LOGN, FB, LT>;
+    auto fn = k_tx<R, LOGN, FB, LT, ZPW>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     if (a.chunk > 1) a.chunk = tx_chunk(a.c.n_sym, a.chunk, Geo<LOGN, BLK>::SPB, resident_blocks(fn, BLK, sm));
@@ -209,6 +209,13 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     if constexpr (LOGN >= 8) {
         // the complex64 register window assumes a cyclic prefix; the complex128 one takes zero padding
         if (a.c.cp <= TPS && (!a.c.zpad || sizeof(R) == 8)) {
+            // complex128 zero padding: the window FIR with the guard compiled in (ZPW)
+            if constexpr (sizeof(R) == 8) {
+                if (a.c.zpad) {
+                    if (a.L <= 4) return tx_launch<R, LOGN, FB, 4, true>(a, grid, s);
+                    if (a.L <= 8) return tx_launch<R, LOGN, FB, 8, true>(a, grid, s);
+                }
+            }
             if (a.L <= 4) return tx_launch<R, LOGN, FB, 4>(a, grid, s);
             if (a.L <= 8) return tx_launch<R, LOGN, FB, 8>(a, grid, s);
         }

@@ -147,12 +147,14 @@ class LinkEngine:
         """Allocate, and hand back to torch's caching allocator, the channel-sample buffers of
         ``runs_in_flight`` concurrent runs of n_sym global symbols (run_pipelined keeps two
         alive), so that later runs reuse them instead of paying for a multi-GB hipMalloc; with
-        lanes > 1, the same on each of run_pipelined's lane streams (the allocator pools buffers
-        per stream)."""
+        lanes > 1, spread over run_pipelined's lane streams (the allocator pools buffers per
+        stream): run k lives on lane k mod lanes, so a lane holds ceil(runs_in_flight / lanes) of
+        them at once -- one each with two lanes."""
         if lanes > 1 and self.device().type == "cuda":
+            per_lane = -(-runs_in_flight // lanes)
             for st in self.lane_streams(lanes):
                 with torch.cuda.stream(st):
-                    self.reserve(n_sym, runs_in_flight, group)
+                    self.reserve(n_sym, per_lane, group)
             return
         world, rank = 1, 0
         if group is not None:

@@ -71,6 +71,12 @@ NOISE_PHASES = 64
 NOISE_MASK = np.uint32(0x1F8)
 SQRT_2LN2 = 1.1774100225154747
 
+# Deviations of a point beyond this many standard deviations of z_stat_bound's model are not
+# expected (the largest of 1e6 Gaussian deviations is ~5 of them; the model's own uncertainty --
+# the receiver's transform taken as no worse than the transmitter's measured one -- is covered by
+# the margin).
+STAT_K = 16.0
+
 
 class Mwc64x:
     """MWC64X (D. B. Thomas): output x ^ c, then (c, x) <- hi / lo of A*x + c.  Vectorised
@@ -200,12 +206,15 @@ class PhiloxLink:
     # (bit_lo, bit_hi, sym_lo, sym_hi): the error counts of every decision consistent with the
     # GPU's deviation from this restatement (decision_bracket), when run_philox(precision=...)
     bracket: Optional[tuple] = None
+    # the same for the per-point statistical deviation scale (run_philox(stat_sigma=...))
+    stat_bracket: Optional[tuple] = None
 
 
 def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq: str, snr_db: float,
                noise_on: bool = True, modulator: str = "OFDM", prefix: str = "CP",
                scheme: str = "QAM", orders=None, precision: Optional[str] = None, radius_fn=None,
-               power_sum: Optional[float] = None) -> PhiloxLink:
+               power_sum: Optional[float] = None, stat_sigma: Optional[float] = None,
+               stat_k: float = STAT_K) -> PhiloxLink:
     """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic.
 
     modulator "OFDM" | "SC" (modulation/models.py:58-91), prefix "CP" | "ZP"
@@ -225,6 +234,13 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     whole-stream sum |y|^2 (its exact fixed-point value), from which sigma is computed as the
     receivers compute it -- together they make the receivers' noise the restatement's bit for bit
     in complex128 (the decision bracket then only covers FFT / FIR / equaliser rounding).
+
+    stat_sigma: the measured per-sample standard deviation of the GPU's transmitted samples from
+    this restatement's (same seed, its transmitter alone; a float, or a function of this
+    restatement's stored samples returning it): also return PhiloxLink.stat_bracket,
+    the decision bracket for a per-point deviation of stat_k standard deviations of the model in
+    z_stat_bound (complex64: the rigorous 2-norm bound of z_error_bound assigns every subcarrier
+    the worst case of the whole transform, c log2(N) u sqrt(N) rms).
     """
     E, tps = geometry(N)
     gen = lane_generators(seed, np.arange(S), N)
@@ -290,13 +306,24 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     Z = O.equalize(Y, H, eq, snr_db)
     if modulator == "SC":
         Z = np.fft.ifft(Z, axis=1, norm="ortho")
-    bracket = None
+    bracket = stat_bracket = None
     if precision is not None:
         delta = z_error_bound(precision, Y, H, eq, snr_db, nerr, modulator, N, np.sqrt(nerr2))
+        dstat = None
+        if stat_sigma is not None:
+            # (a callable gets the stored samples -- (S, N + cp) with zero padding, else (S, N) -- and
+            # returns the measured deviation of the GPU's from them)
+            sig = stat_sigma(y if prefix == "ZP" else yk) if callable(stat_sigma) else float(stat_sigma)
+            dstat = z_stat_bound(precision, Y, H, eq, snr_db, sig, np.sqrt(np.mean(np.abs(yk) ** 2)),
+                                 modulator, N, stat_k)
         if orders is not None:
             bracket = adaptive_bracket(Z, idx, orders, bk, delta, scheme)
+            if dstat is not None:
+                stat_bracket = adaptive_bracket(Z, idx, orders, bk, dstat, scheme)
         else:
             bracket = decision_bracket(Z, idx, lut, b, delta, scheme)
+            if dstat is not None:
+                stat_bracket = decision_bracket(Z, idx, lut, b, dstat, scheme)
     if orders is not None:
         ridx = np.zeros((S, N), np.int64)
         for o, lt in luts.items():
@@ -304,12 +331,12 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
             ridx[:, cols] = O.nn_demap(Z[:, cols].ravel(), lt).reshape(S, len(cols))
         diff = (ridx ^ idx).astype(np.int64)
         be, se = adaptive_counts(diff, bk, S)
-        return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk, bracket)
+        return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk, bracket, stat_bracket)
     ridx = O.nn_demap(Z.ravel(), lut).reshape(S, N)
     diff = (ridx ^ idx).astype(np.uint64)
     be = int(sum(int(np.count_nonzero((diff >> np.uint64(j)) & np.uint64(1))) for j in range(b)))
     se = int(np.count_nonzero(ridx != idx))
-    return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk, bracket)
+    return PhiloxLink(be, se, py, px, mx, idx, y if prefix == "ZP" else yk, bracket, stat_bracket)
 
 
 def adaptive_counts(diff: np.ndarray, bk: np.ndarray, S: int):
@@ -380,6 +407,45 @@ def z_error_bound(precision: str, Y: np.ndarray, H: np.ndarray, eq: str, snr_db:
         d = g.max(axis=1) * e2 + (rel + 6.0 * logn * u) * z2 + 1e-300
         d = np.broadcast_to(d[:, None], (S, N))
     return np.asarray(d)
+
+
+def z_stat_bound(precision: str, Y: np.ndarray, H: np.ndarray, eq: str, snr_db: float, sigma_tx: float,
+                 rms_y: float, modulator: str, N: int, k: float = STAT_K) -> np.ndarray:
+    """(S, N) per-point deviation scale of the GPU's equalised points from this restatement's: k
+    times the standard deviation of a model calibrated by the GPU's own transmitter.
+
+    sigma_tx is the measured per-sample standard deviation of the GPU's channel samples from the
+    restatement's (its IFFT, FIR and stores).  The receiver adds the noise product's rounding (u
+    rms(y)) and its FFT, taken to deviate no more than the transmitter (which carries an IFFT and
+    the FIR), so a received sample deviates by sd_t = sqrt(2 sigma_tx^2 + (u rms_y)^2) per sample;
+    the ortho FFT preserves it per subcarrier.  The equaliser multiplies it by the subcarrier's gain
+    g (ZF 1/|H|, MMSE |H| / (|H|^2 + nv)) and adds a few roundings of |Z| (8 u; MMSE: its noise
+    variance from the GPU's own received power, relative 2 sd_t / rms).  Single carrier: the IFFT
+    after the equaliser spreads the subcarriers' deviations over every sample, sqrt(mean g^2) sd_t,
+    plus its own rounding (sd_t relative to the equalised signal)."""
+    S = Y.shape[0]
+    u = 2.0 ** -24 if precision == "f32" else 2.0 ** -53
+    sd_t = np.sqrt(2.0 * sigma_tx ** 2 + (u * rms_y) ** 2)
+    rms = np.sqrt(np.mean(np.abs(Y) ** 2, axis=1))
+    if eq == "NONE":
+        g = np.ones((S, N))
+        rel = 0.0
+    elif eq == "ZF":
+        h = np.where(H == 0, 1e-10, H)
+        g = np.broadcast_to(1.0 / np.abs(h), (S, N))
+        rel = 8 * u
+    else:
+        gm = np.mean(np.abs(H) ** 2)
+        nv = (np.mean(np.abs(Y) ** 2, axis=1) / 10 ** (snr_db / 10)) / gm
+        g = np.abs(H)[None, :] / (np.abs(H)[None, :] ** 2 + nv[:, None])
+        rel = 8 * u + 2 * sd_t / np.maximum(np.max(rms), 1e-300)
+    Zabs = np.abs(Y) * g
+    d = g * sd_t + rel * Zabs
+    if modulator == "SC":
+        zr = np.sqrt(np.mean(Zabs ** 2, axis=1))
+        d = np.sqrt(np.mean(g ** 2, axis=1)) * sd_t + (rel + sd_t / np.maximum(np.max(rms), 1e-300)) * zr
+        d = np.broadcast_to(d[:, None], (S, N))
+    return k * np.asarray(d) + 1e-300
 
 
 def _qam_levels(lut: np.ndarray):

@@ -16,7 +16,7 @@ import re
 import sys
 from collections import Counter, defaultdict
 
-REG = re.compile(r"\b([vs])(?:\[(\d+):(\d+)\]|(\d+))\b")
+REG = re.compile(r"\b([vs])(?:\[(\d+):(\d+)\]|(\d+)\b)")  # (no \b after "]": ranges were missed)
 NODEF = re.compile(r"^(ds_write|ds_bpermute_b32_no|global_store|buffer_store|scratch_store|flat_store|"
                    r"v_cmp|v_cmpx|s_|exp|ds_gws|global_atomic(?!.*glc)|buffer_atomic(?!.*glc))")
 
@@ -156,10 +156,21 @@ def main():
     print(f"peak live VGPRs {peak} at block {blocks[i]['label']} ins {k}: {blocks[i]['ins'][k][0]}  ({blocks[i]['ins'][k][1]})")
     for j in range(max(0, k - 4), min(len(blocks[i]["ins"]), k + 3)):
         print("   ", blocks[i]["ins"][j][0], " ", blocks[i]["ins"][j][1])
+    # attribute each live register to its nearest preceding definition in program order (straight-
+    # line code: the reaching definition; registers are reused, so "the line that most often
+    # defines it" misleads)
+    flat = [(bi, ki) for bi, b in enumerate(blocks) for ki in range(len(b["ins"]))]
+    pos = flat.index((i, k))
     groups = Counter()
     for r in ls:
-        groups[defloc[r].most_common(1)[0][0] if defloc[r] else "(entry)"] += 1
-    print("live set by defining source line (most registers first):")
+        src = "(entry / loop-carried)"
+        for q in range(pos, -1, -1):
+            bi, ki = flat[q]
+            if r in info[bi][ki][0]:
+                src = blocks[bi]["ins"][ki][1]
+                break
+        groups[src] += 1
+    print("live set by reaching (nearest preceding) definition's source line:")
     for loc, n in groups.most_common(top):
         print(f"   {n:4d}  {loc}")
 
