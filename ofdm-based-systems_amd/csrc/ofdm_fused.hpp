@@ -341,6 +341,10 @@ constexpr int rx_waves() {
 }
 // throughput RX: equaliser coefficients staged in LDS up to N = 2^OFDM_EQ_LDS_MAX_LOGN (beyond,
 // the table would cost a resident workgroup per CU)
+// adaptive RX: the partial-byte path reads the subcarrier table through an opaque pointer (A/B switch)
+#ifndef OFDM_ADAPT_OPAQUE_SC
+#define OFDM_ADAPT_OPAQUE_SC 0
+#endif
 #ifndef OFDM_EQ_LDS_MAX_LOGN
 #define OFDM_EQ_LDS_MAX_LOGN 11
 #endif
@@ -1473,7 +1477,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                         // for a branch only the run's last symbol takes.)
                         static_assert(sizeof(ScInfo) == 8, "ScInfo is one 8-byte word");
                         gptr<const uint64_t> scp = (gptr<const uint64_t>)cm.sc;
-                        asm volatile("" : "+s"(scp));
+                        if (OFDM_ADAPT_OPAQUE_SC) asm volatile("" : "+s"(scp));
                         uint32_t vm = 0;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {

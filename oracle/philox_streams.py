@@ -275,16 +275,16 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     else:
         yk, tail = y[:, cp:].copy(), None
     rxs = yk.copy()
-    nerr = np.zeros(S)  # per symbol: sum over its received samples of the noise deviation bound
-    nerr2 = np.zeros(S)  # ... and the sum of its squares
+    # per received sample: the bound on the GPU's noise deviation (zero padding: a guard-tail sample's
+    # own bound adds onto the bound of the sample it is overlap-added to, before the per-symbol sums)
+    nbs = np.zeros((S, N))
     if noise_on:
         # sigma^2 = mean |y|^2 / snr (noise/models.py:13-18), as k_rx evaluates it in double
         p = (py if power_sum is None else float(power_sum)) / (S * (N + cp))
         sigma = float(np.sqrt((p / 10 ** (snr_db / 10)) / 2.0))
         if want_bound:
             nz, nb = lane_noise(gen, S, N, sigma, with_bound=True, radius_fn=radius_fn, product_rel=prel)
-            nerr += nb.sum(axis=1)
-            nerr2 += (nb ** 2).sum(axis=1)
+            nbs += nb
         else:
             nz = lane_noise(gen, S, N, sigma, radius_fn=radius_fn)
         rxs = rxs + nz
@@ -298,9 +298,10 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
                 use = k < cp
                 srow = np.repeat(np.arange(S), tps)[use]
                 tail[srow, k[use]] += n[use]
-                np.add.at(nerr, srow, nb[use])
-                np.add.at(nerr2, srow, nb[use] ** 2)
+                np.add.at(nbs, (srow, k[use]), nb[use])
         rxs[:, :cp] += tail
+    nerr = nbs.sum(axis=1)  # per symbol: sum over its received samples of the deviation bound
+    nerr2 = (nbs ** 2).sum(axis=1)  # ... and the sum of its squares (the 2-norm of the deviations)
     H = np.fft.fft(np.asarray(h_raw, np.complex128), N)
     Y = np.fft.fft(rxs, axis=1, norm="ortho")
     Z = O.equalize(Y, H, eq, snr_db)

@@ -35,7 +35,7 @@ def kernel_key(name: str):
     args = [a.strip() for a in name[name.index("<") + 1:name.index(">")].split(",")]
     if "k_rx" in name and len(args) >= 4 and int(args[3]) > 0:  # k_rx<R, LOGN, EQ, FB, MV>
         return "ofdm_rx"
-    if "k_tx" in name and len(args) == 4 and int(args[2]) > 0:
+    if "k_tx" in name and len(args) >= 4 and int(args[2]) > 0:  # k_tx<R, LOGN, FB, LT, ZPW>
         return "ofdm_tx"
     return None
 
