@@ -1355,6 +1355,53 @@ struct Mwc64x {
     }
 };
 
+// A workgroup prologue's copy of a global table into LDS, split into load() and store() so that
+// a kernel issues the reads of all its tables before the first wait: each copy loop waited for
+// its own loads (global_load, s_waitcnt vmcnt(0), ds_write per trip), and the prologues of the
+// fused kernels chained five or six memory latencies, ~4 us per workgroup.  The first K trips
+// of each thread are held in registers; a longer table (MAXN > 8 BLK, or a count not bounded by
+// MAXN: BOUNDED false) copies its remainder in store().  The caller syncs.
+#ifndef OFDM_STAGED_PROLOGUE
+#define OFDM_STAGED_PROLOGUE 1
+#endif
+template <int BLK, int MAXN, typename T, bool BOUNDED = true>
+struct Staged {
+    static constexpr int K = MAXN <= 0 ? 0 : ((MAXN + BLK - 1) / BLK < 8 ? (MAXN + BLK - 1) / BLK : 8);
+    T v[K > 0 ? K : 1];
+    const T* src = nullptr;
+    int n = 0;
+    __device__ __forceinline__ void load(const T* s, int cnt) {
+        src = s;
+        n = cnt;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = (int)threadIdx.x + k * BLK;
+            if (i < n) v[k] = s[i];
+        }
+    }
+    template <class F>
+    __device__ __forceinline__ void store(T* dst, F f) const {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = (int)threadIdx.x + k * BLK;
+            if (i < n) dst[i] = f(v[k]);
+        }
+        if constexpr (!BOUNDED || MAXN > K * BLK)
+            for (int i = (int)threadIdx.x + K * BLK; i < n; i += BLK) dst[i] = f(src[i]);
+    }
+    __device__ __forceinline__ void store(T* dst) const {
+        store(dst, [](const T& x) { return x; });
+    }
+};
+
+// a struct's bytes as dwords: staged as such, a struct of byte arrays (AxisInfo) is copied with
+// its loads' registers as they are, not split into bytes and packed again
+template <typename T>
+struct Dwords {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized");
+    uint32_t w[sizeof(T) / 4];
+};
+
 // Build the noise phase table in LDS (threads < 64; caller syncs); ntab64 (complex128 kernels,
 // or null): the same float32 entries widened to double.
 __device__ __forceinline__ void build_noise_table(f32x2* ntab, double sigma, f64x2* ntab64 = nullptr) {

@@ -150,6 +150,11 @@ constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && L
 // VGPR, the element offsets in SGPRs) instead of four 64-bit VGPR addresses (RX b 3.09 -> 3.06,
 // c 3.75 -> 3.70 ms per step at the same occupancy, profiles/r03ab_ab.txt)
 
+// complex128 window-FIR TX (A/B): the outputs stored from the lanes' registers instead of through
+// the row (lane-contiguous: 64 lines per store instruction)
+#ifndef OFDM_FIR_DIRECT_STORE
+#define OFDM_FIR_DIRECT_STORE 0
+#endif
 // complex128 window-FIR TX: the window's LDS reads chained to the samples before them (see k_tx)
 #ifndef OFDM_FIR_STREAM
 #define OFDM_FIR_STREAM 0
@@ -354,6 +359,20 @@ template <typename R, int FB, int LOGN, int EQ>
 constexpr bool eq_in_lds() {
     return FB > 0 && EQ > OFDM_EQ_NONE && LOGN <= (sizeof(R) == 8 ? 12 : OFDM_EQ_LDS_MAX_LOGN) &&
            !f64_rx_solo<R, FB, LOGN>();
+}
+// complex128 throughput receivers at N = 1024 (configs b, c): one workgroup holds a CU, and each
+// start and drain of one idles it -- the grid is OFDM_RX_GRID_ROUNDS rounds of the resident
+// workgroups instead of up to kMaxGrid.  Config c RX 3.556 -> 3.50 ms per 1e6 symbols and
+// 0.43 -> 0.37 ms per 1e5 (a sweep point); one round (static striding) lost 2 % at 1e6, and the
+// other receivers (several workgroups per CU) lost 1-5 % with two (profiles/r05h_ab_grid_resident.txt).
+// (A queue the waves took their symbols from was 3.4x slower: one atomic counter serialised
+// ~12 ns per symbol, profiles/r05j_ab_rx_symbol_queue.txt.)
+#ifndef OFDM_RX_GRID_ROUNDS
+#define OFDM_RX_GRID_ROUNDS 2
+#endif
+template <typename R, int FB, int LOGN>
+constexpr int rx_grid_rounds() {
+    return sizeof(R) == 8 && FB > 0 && LOGN == 10 ? OFDM_RX_GRID_ROUNDS : 0;
 }
 // the lane's coefficients loaded after the FFT (in flight across the MMSE power reduction)
 template <typename R, int FB, int LOGN, int EQ>
@@ -585,38 +604,87 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
     // subcarriers point at a zero entry appended to the LUT pool
     uint32_t* sce = cv.take<uint32_t>(FB == 1 ? N : 0);
 
+    // the tables' global reads issued first (Staged), then the LDS writes
+    constexpr bool FOLD_H0 = FB > 0 && LT == 0;
+    const C* glut = (const C*)cm.lut;
+    Staged<BLK, TTS, C> st_tt;
+    Staged<BLK, (FB > 0 ? LUT_STATIC : BLK), C, (FB > 0)> st_lut;  // (generic kernel: any LUT length)
+    Staged<BLK, (FB == 1 ? N : 0), ScInfo> st_sc;
+    Staged<BLK, kMaxLuts, Dwords<AxisInfo>> st_ax;
+    static_assert(kMaxLuts <= BLK && 32 <= BLK, "one axis entry / tap per thread");
+    C hq = mk<R>(0, 0), sep_a = mk<R>(0, 0), sep_b = mk<R>(0, 0), hf = mk<R>(1, 0);
+    int ax_off = 0;
+    if (OFDM_STAGED_PROLOGUE) {
+        if constexpr (FOLD_H0) hf = ((const C*)a.h)[0];
+        st_tt.load((const C*)cm.ptw + TTS, TTS);
+        st_lut.load(glut, cm.lut_len);
+        if constexpr (FB == 1) st_sc.load(cm.sc, N);
+        st_ax.load((const Dwords<AxisInfo>*)cm.axis, cm.n_axis);
+        if (threadIdx.x < L && threadIdx.x < 32) hq = ((const C*)a.h)[threadIdx.x];
+        // adaptive: lane l of every wave holds order l's LUT offset, for the codes' lane shuffle
+        if constexpr (FB == 1) {
+            if ((int)(threadIdx.x & 63) < cm.n_axis) ax_off = cm.axis[threadIdx.x & 63].lut_off;
+        }
+        if constexpr (SEP) {
+            if (threadIdx.x < SIDE) sep_a = glut[threadIdx.x], sep_b = glut[threadIdx.x << HB];
+        }
+    }
     if constexpr (!TT) load_twiddles<R>(tw, (const C*)cm.tw);
-    for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
     // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element);
     // flat throughput kernel: the channel tap too (y = h0 ifft(X) = ifft(h0 X)), so the
     // symbol leaves the IFFT as the channel output
-    constexpr bool FOLD_H0 = FB > 0 && LT == 0;
     const R lut_scale = scm ? (R)1 : (R)cm.scale;
-    const C hf = FOLD_H0 ? ((const C*)a.h)[0] : mk<R>(1, 0);
-    for (int i = threadIdx.x; i < cm.lut_len; i += BLK)
-        lut[i] = cscale(FOLD_H0 ? cmul(hf, ((const C*)cm.lut)[i]) : ((const C*)cm.lut)[i], lut_scale);
-    if constexpr (SEP) {
-        // LUT[i] = I[i & (SIDE - 1)] + j Q[i >> HB] exactly (the plan's build_axis verified it):
-        // I from the entries with Q index 0, Q from those with I index 0, the same scaled values
-        if (threadIdx.x < SIDE) {
-            sep_s[threadIdx.x] = ((const C*)cm.lut)[threadIdx.x].re * lut_scale;
-            sep_s[SIDE + threadIdx.x] = ((const C*)cm.lut)[threadIdx.x << HB].im * lut_scale;
+    if (OFDM_STAGED_PROLOGUE) {
+        st_tt.store(tt);
+        st_lut.store(lut, [&](const C& v) { return cscale(FOLD_H0 ? cmul(hf, v) : v, lut_scale); });
+        if constexpr (SEP) {
+            // LUT[i] = I[i & (SIDE - 1)] + j Q[i >> HB] exactly (the plan's build_axis verified it):
+            // I from the entries with Q index 0, Q from those with I index 0, the same scaled values
+            if (threadIdx.x < SIDE) {
+                sep_s[threadIdx.x] = sep_a.re * lut_scale;
+                sep_s[SIDE + threadIdx.x] = sep_b.im * lut_scale;
+            }
         }
+        st_ax.store((Dwords<AxisInfo>*)axis);
+    } else {
+        for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
+        if constexpr (FOLD_H0) hf = ((const C*)a.h)[0];
+        for (int i = threadIdx.x; i < cm.lut_len; i += BLK)
+            lut[i] = cscale(FOLD_H0 ? cmul(hf, glut[i]) : glut[i], lut_scale);
+        if constexpr (SEP) {
+            if (threadIdx.x < SIDE) {
+                sep_s[threadIdx.x] = glut[threadIdx.x].re * lut_scale;
+                sep_s[SIDE + threadIdx.x] = glut[threadIdx.x << HB].im * lut_scale;
+            }
+        }
+        if (threadIdx.x < L && threadIdx.x < 32) hq = ((const C*)a.h)[threadIdx.x];
+        if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     }
     if constexpr (FB == 1) {
         if (threadIdx.x == 0) lut[cm.lut_len] = mk<R>(0, 0);
-        for (int k = threadIdx.x; k < N; k += BLK) {
+        auto code = [&](const ScInfo& sc, int off) {
+            return sc.lut < 0 ? (uint32_t)cm.lut_len << 8 : ((uint32_t)off << 8) | ((1u << sc.bits) - 1u);
+        };
+        int k0 = threadIdx.x;
+        if (OFDM_STAGED_PROLOGUE) {
+            // the order's LUT offset from the lane holding it (a read per element, dependent on
+            // the staged entry, waited for one by one)
+#pragma unroll
+            for (int q = 0; q < st_sc.K; ++q, k0 += BLK) {
+                const ScInfo sc = st_sc.v[q];
+                const int off = __shfl(ax_off, sc.lut < 0 ? 0 : (int)sc.lut);
+                if (k0 < N) sce[k0] = code(sc, off);
+            }
+        }
+        for (int k = k0; k < N; k += BLK) {
             const ScInfo sc = cm.sc[k];
-            sce[k] = sc.lut < 0 ? (uint32_t)cm.lut_len << 8
-                                : ((uint32_t)cm.axis[sc.lut].lut_off << 8) | ((1u << sc.bits) - 1u);
+            sce[k] = code(sc, sc.lut < 0 ? 0 : cm.axis[sc.lut].lut_off);
         }
     }
     if (threadIdx.x < 32) {
-        const C hq = threadIdx.x < L ? ((const C*)a.h)[threadIdx.x] : mk<R>(0, 0);
         h[threadIdx.x] = hq;
         if (WFIR) hsw[threadIdx.x] = mk<R>(-hq.im, hq.re);  // window FIR (complex64): taps swizzled
     }
-    if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     __syncthreads();
 
     const int ls = TPS >= 64 ? __builtin_amdgcn_readfirstlane(threadIdx.x / TPS) : threadIdx.x / TPS;
@@ -946,6 +1014,20 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
                                 pys = __builtin_fma(pi, pi, pys);
                             }
                         }
+                        if constexpr (OFDM_FIR_DIRECT_STORE && TPS >= 64) {
+                            // (A/B) the lane's 8 consecutive outputs stored from the registers: 8 store
+                            // instructions of 64 distinct 128-byte lines each, no LDS transpose
+                            C* yh = yout + sl * ystride + h * NH;
+                            gptr<C> yg = lane_ptr(uniform_ptr(yh), (uint32_t)(8 * to));
+#pragma unroll
+                            for (int j = 0; j < 8; ++j) {
+                                const C yv = mk<R>(T[j] - U[j], T[j] + V[j]);
+                                pys = __builtin_fma(yv.re, yv.re, pys);
+                                pys = __builtin_fma(yv.im, yv.im, pys);
+                                if (store) st_stream<false>(yg + j, yv);
+                            }
+                            return;
+                        }
                         sym_sync<TPS>();  // every window is read: the outputs take the row
 #pragma unroll
                         for (int j = 0; j < 8; ++j) {
@@ -1186,6 +1268,16 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     constexpr bool EQ_REG = EQ_PRE || EQ_LATE;  // coefficients in registers (ecoef)
     constexpr bool MMSE_BATCH = sizeof(R) == 8 && FB > 1 && EQ == OFDM_EQ_MMSE;
 
+    // the tables' global reads issued first (Staged), the noise table built while they fly
+    Staged<BLK, (FB > 1 && MV ? 2 : 1) * TTS, C> st_tt;
+    Staged<BLK, EQ_LDS ? N : 0, C> st_eq;
+    Staged<BLK, kMaxLuts, Dwords<AxisInfo>> st_ax;
+    static_assert(kMaxLuts <= BLK, "one axis entry per thread");
+    if (OFDM_STAGED_PROLOGUE) {
+        st_tt.load((const C*)cm.ptw, tts_all);
+        if constexpr (EQ_LDS) st_eq.load((const C*)cm.eq_a, N);
+        st_ax.load((const Dwords<AxisInfo>*)cm.axis, cm.n_axis);
+    }
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     const bool noise = a.noise_on && !(flags & 1);
     double sigma_d = 0;
@@ -1196,15 +1288,21 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     const R sigma = (R)sigma_d;
     build_noise_table(ntab, sigma_d, ntab64);
     if constexpr (!TT) load_twiddles<R>(tw, (const C*)cm.tw);
-    for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
-    if constexpr (EQ_LDS)
-        for (int k = threadIdx.x; k < N; k += BLK) eqt[k] = ((const C*)cm.eq_a)[k];
-    if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
+    if (OFDM_STAGED_PROLOGUE) {
+        st_tt.store(tt);
+        if constexpr (EQ_LDS) st_eq.store(eqt);
+        st_ax.store((Dwords<AxisInfo>*)axis);
+    } else {
+        for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
+        if constexpr (EQ_LDS)
+            for (int k = threadIdx.x; k < N; k += BLK) eqt[k] = ((const C*)cm.eq_a)[k];
+        if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
+    }
     if constexpr (FB == 1 && sizeof(R) == 8) {
         if (threadIdx.x < 8) {
             OrderParams64 o = OrderParams64::make(0.0, 0.0, 0.0, 0u);  // unused subcarrier: level 0, no bits
             if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
-                const AxisInfo ax = cm.axis[threadIdx.x];
+                const AxisInfo ax = OFDM_STAGED_PROLOGUE ? __builtin_bit_cast(AxisInfo, st_ax.v[0]) : cm.axis[threadIdx.x];
                 const double span = (double)(ax.side - 1);
                 o = OrderParams64::make(ax.inv_step * cm.scale / span,  // mul: the FFT output stays unscaled
                                         ax.lev0 * ax.inv_step / span,   // add: negated in the FMA
@@ -1217,7 +1315,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
             // unused subcarrier: level 0, no bits
             OrderParams o{0.f, 0.f, 0u, 0u};
             if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
-                const AxisInfo ax = cm.axis[threadIdx.x];
+                const AxisInfo ax = OFDM_STAGED_PROLOGUE ? __builtin_bit_cast(AxisInfo, st_ax.v[0]) : cm.axis[threadIdx.x];
                 const double span = (double)(ax.side - 1);  // see OrderParams
                 o.mul = (float)(ax.inv_step * cm.scale / span);  // the FFT output stays unscaled
                 o.add = (float)(-ax.lev0 * ax.inv_step / span);

@@ -168,6 +168,17 @@ static inline int tx_chunk(int64_t n_sym, int max_chunk, int spb, int resident) 
     return best;
 }
 
+// OFDM_GRID_RESIDENT k > 0 (A/B): the fused receiver's grid capped at k x the workgroups resident at
+// once, so each workgroup stages its tables once and loops over its share of the symbols (the
+// transmitter lost 4-8 % that way: profiles/r05h_ab_grid_resident.txt)
+#ifndef OFDM_GRID_RESIDENT
+#define OFDM_GRID_RESIDENT 0
+#endif
+static inline int fused_grid(int64_t want, int resident) {
+    if (OFDM_GRID_RESIDENT > 0 && resident > 0) want = std::min<int64_t>(want, (int64_t)OFDM_GRID_RESIDENT * resident);
+    return clamp_grid(want);
+}
+
 template <typename R, int LOGN, int FB, int LT, bool ZPW = false>
 static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     constexpr int BLK = tx_block<R, FB, LOGN, LT, ZPW>();
@@ -194,7 +205,8 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     auto fn = k_tx<R, LOGN, FB, LT, ZPW>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
-    if (a.chunk > 1) a.chunk = tx_chunk(a.c.n_sym, a.chunk, Geo<LOGN, BLK>::SPB, resident_blocks(fn, BLK, sm));
+    const int resident = resident_blocks(fn, BLK, sm);
+    if (a.chunk > 1) a.chunk = tx_chunk(a.c.n_sym, a.chunk, Geo<LOGN, BLK>::SPB, resident);
     const int64_t groups = (a.c.n_sym + a.chunk - 1) / a.chunk;
     *grid = clamp_grid((groups + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
@@ -291,7 +303,11 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     auto fn = k_rx<R, LOGN, EQ, FB, MV>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
-    *grid = clamp_grid((a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB);
+    const int64_t want = (a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB;
+    constexpr int ROUNDS = rx_grid_rounds<R, FB, LOGN>();
+    const int res = ROUNDS > 0 ? resident_blocks(fn, BLK, sm) : 0;
+    *grid = res > 0 ? clamp_grid(std::min<int64_t>(want, (int64_t)ROUNDS * res))
+                    : fused_grid(want, OFDM_GRID_RESIDENT > 0 ? resident_blocks(fn, BLK, sm) : 0);
     hipLaunchKernelGGL(fn, dim3(*grid), dim3(BLK), sm, s, a);
     return hipGetLastError();
 }
