@@ -203,10 +203,12 @@ int psk_order(const double* lut, int m) {
 
 // Multipath TX: consecutive OFDM symbols per symbol group; the group's first symbol regenerates
 // its predecessor's tail (one extra bits + map + IFFT per group).  32 against 16: complex128 TX
-// c 5.15 -> 5.00, d 5.24 -> 5.04, e 5.19 -> 5.00 ms per step; 64 leaves a ragged last round of
-// workgroups and measured slower than 32 (profiles/r03ag_ab.txt)
+// c 5.15 -> 5.00, d 5.24 -> 5.04, e 5.19 -> 5.00 ms per step (profiles/r03ag_ab.txt).  Since each
+// launch picks its chunk in [max / 2, max] to fill whole rounds of resident workgroups (tx_chunk),
+// 64 (64 against 32: TX d 4.53 -> 4.44 ms, c and e within 0.5 %; 128: d 4.40, c and e 1 % slower
+// and the 1e5-symbol sweep points 20 %, profiles/r05n_ab_tx_chunk.txt)
 #ifndef OFDM_TX_CHUNK
-#define OFDM_TX_CHUNK 32
+#define OFDM_TX_CHUNK 64
 #endif
 
 #if OFDM_ABLATION

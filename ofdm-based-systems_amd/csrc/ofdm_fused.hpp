@@ -374,6 +374,10 @@ template <typename R, int FB, int LOGN>
 constexpr int rx_grid_rounds() {
     return sizeof(R) == 8 && FB > 0 && LOGN == 10 ? OFDM_RX_GRID_ROUNDS : 0;
 }
+// the complex128 adaptive receiver's MMSE with the four-element batched reciprocal as well (A/B)
+#ifndef OFDM_MMSE_BATCH_ADAPT
+#define OFDM_MMSE_BATCH_ADAPT 1
+#endif
 // the lane's coefficients loaded after the FFT (in flight across the MMSE power reduction)
 template <typename R, int FB, int LOGN, int EQ>
 constexpr bool rx_eq_late() { return f64_rx_solo<R, FB, LOGN>() && EQ > OFDM_EQ_NONE; }
@@ -1266,7 +1270,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     constexpr bool EQ_PRE =
         !EQ_LDS && !EQ_LATE && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
     constexpr bool EQ_REG = EQ_PRE || EQ_LATE;  // coefficients in registers (ecoef)
-    constexpr bool MMSE_BATCH = sizeof(R) == 8 && FB > 1 && EQ == OFDM_EQ_MMSE;
+    constexpr bool MMSE_BATCH = sizeof(R) == 8 && FB > 0 && EQ == OFDM_EQ_MMSE && OFDM_MMSE_BATCH_ADAPT >= (FB == 1);
 
     // the tables' global reads issued first (Staged), the noise table built while they fly
     Staged<BLK, (FB > 1 && MV ? 2 : 1) * TTS, C> st_tt;
@@ -1543,6 +1547,32 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                 if (scm || eq == OFDM_EQ_NONE) return x[i];  // single carrier: equalised before the IFFT
                 return eq_apply(x[i], t + i * TPS, nv, &ecoef[EQ_REG ? i : 0]);
             };
+            // MMSE in complex128: conj(H) v / (|H|^2 + nv) of a lane word's four elements, the four
+            // reciprocals from one (MMSE_BATCH)
+            auto mmse4 = [&](int q, C(&z)[4]) {
+                C c[4];
+                R dn[4], inv[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    c[j] = EQ_LDS ? eqt[t + (4 * q + j) * TPS] : ecoef[EQ_REG ? 4 * q + j : 0];
+                    dn[j] = c[j].re * c[j].re + c[j].im * c[j].im + nv;
+                }
+                const R p01 = dn[0] * dn[1], p012 = p01 * dn[2], p = p012 * dn[3];
+                if (__builtin_expect(p >= (R)1e-280 && p <= (R)1e280, 1)) {
+                    R r = recip<R>(p);  // 1 / (d0 d1 d2 d3)
+                    inv[3] = r * p012;
+                    r *= dn[3];  // 1 / (d0 d1 d2)
+                    inv[2] = r * p01;
+                    r *= dn[2];  // 1 / (d0 d1)
+                    inv[1] = r * dn[0];
+                    inv[0] = r * dn[1];
+                } else {  // a zero, infinite or extreme factor: one reciprocal each
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) inv[j] = recip<R>(dn[j]);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) z[j] = cscale(cmul(x[4 * q + j], c[j]), inv[j]);
+            };
             if constexpr (FB == 1) {
                 // four elements per lane word, each through its subcarrier's order (the codes
                 // are made opaque per symbol: the order-table reads stay inside the loop)
@@ -1553,11 +1583,15 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                     const OP* op[4];
                     uint32_t oc = ocode[q];
                     asm volatile("" : "+v"(oc));
+                    if (MMSE_BATCH) {
+                        mmse4(q, z);
+                    } else {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        z[j] = equalized(4 * q + j);
-                        op[j] = (const OP*)((const unsigned char*)ordt + ((oc >> (8 * j)) & 0xFFu));
+                        for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
                     }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        op[j] = (const OP*)((const unsigned char*)ordt + ((oc >> (8 * j)) & 0xFFu));
                     uint32_t d;
                     if constexpr (sizeof(R) == 8)
                         d = small_orders ? adaptive_diff64<true>(z, op, lane_word(tb.lane, q), magic64)
@@ -1598,29 +1632,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                     }
                     C z[4];
                     if (MMSE_BATCH && !scm) {
-                        // conj(H) v / (|H|^2 + nv) with the four reciprocals from one
-                        C c[4];
-                        R dn[4], inv[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            c[j] = EQ_LDS ? eqt[t + (4 * q + j) * TPS] : ecoef[EQ_REG ? 4 * q + j : 0];
-                            dn[j] = c[j].re * c[j].re + c[j].im * c[j].im + nv;
-                        }
-                        const R p01 = dn[0] * dn[1], p012 = p01 * dn[2], p = p012 * dn[3];
-                        if (__builtin_expect(p >= (R)1e-280 && p <= (R)1e280, 1)) {
-                            R r = recip<R>(p);  // 1 / (d0 d1 d2 d3)
-                            inv[3] = r * p012;
-                            r *= dn[3];  // 1 / (d0 d1 d2)
-                            inv[2] = r * p01;
-                            r *= dn[2];  // 1 / (d0 d1)
-                            inv[1] = r * dn[0];
-                            inv[0] = r * dn[1];
-                        } else {  // a zero, infinite or extreme factor: one reciprocal each
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) inv[j] = recip<R>(dn[j]);
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) z[j] = cscale(cmul(x[4 * q + j], c[j]), inv[j]);
+                        mmse4(q, z);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
