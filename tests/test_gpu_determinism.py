@@ -66,3 +66,30 @@ def test_full_size_runs_repeat_their_counts(gpu, cfg):
     assert a.bit_errors > 0
     assert (a.bit_errors, a.symbol_errors, a.power_sum) == (b.bit_errors, b.symbol_errors, b.power_sum)
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("cfg,S,split", SHAPES, ids=[s[0] for s in SHAPES])
+def test_full_size_rx_halves_add_up_to_the_whole(gpu, cfg, S, split):
+    """The receiver over [0, S) and over [0, split) + [split, S) of one transmitted stream count the
+    same errors: every symbol is decided exactly once whatever the launch's grid (the N = 1024
+    receivers stride a grid of two resident rounds, the others up to kMaxGrid workgroups)."""
+    N, M, ch, ratio, eq, snr, _ = bench.CONFIGS[cfg]
+    eng = bench.make_engine(bench.CONFIGS[cfg], "f64")
+    seed = 777
+    y = torch.empty((S, eng.ystride), dtype=eng.cdtype, device="cuda")
+    stats = new_stats("cuda")
+    st = eng.stream()
+    eng.tx(st, None, seed, 0, S, y, stats)
+    samples = S * (N + eng.cp)
+    n_valid = eng.valid_bits(S)
+    whole = torch.zeros(2, dtype=torch.int64, device="cuda")
+    eng.rx(st, y, None, None, seed, stats, samples, snr, True, None, 0, S, n_valid, whole)
+    parts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    eng.rx(st, y[:split], None, None, seed, stats, samples, snr, True, None, 0, split, n_valid, parts)
+    eng.rx(st, y[split:], None, None, seed, stats, samples, snr, True, None, split, S - split, n_valid, parts)
+    torch.cuda.synchronize()
+    w, p = whole.cpu().tolist(), parts.cpu().tolist()
+    assert w[0] > 0
+    assert w == p, f"config {cfg}: whole {w} != halves {p}"
+    del y
+    torch.cuda.empty_cache()
