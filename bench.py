@@ -446,59 +446,101 @@ def reference_sweep(engine64, N, cp, snrs, symbols):
     return out
 
 
-def measure_sweep(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory):
-    """The SNR sweep as the bench step: every step runs all SWEEP_GRID points, `per_gpu` OFDM
-    symbols per GPU each (one complete run per point, new seed per point and step), pipelined
-    through LinkEngine.run_pipelined and symbol-sharded across ranks; W untimed steps, K timed."""
-    N = cfg[0]
-    engine = factory(cfg, precision)
+# The sweeps of BASELINE configs[2..4] as the reference's settings files run them (SURVEY 8(d)): one
+# engine (plan) per group, each group's SNR points pipelined through LinkEngine.run_pipelined.
+#   c: config/simulation_settings_custom_channel.json's channel at N = 1024 / 64-QAM over SWEEP_GRID;
+#   d: config/simulation_settings_adaptive.json's SNRs 15 / 20 / 25 dB (the bit loading is derived
+#      per SNR, simulation/models.py:289-395, so every point has its own plan);
+#   e: config/simulation_settings_waterfilling.json's SNRs 10..30 dB by 5 at 16-, 64- and 256-QAM
+#      (BASELINE configs[4]: "up to 256-QAM").
+SWEEP_SNRS_D = [15.0, 20.0, 25.0]
+SWEEP_SNRS_E = [10.0, 15.0, 20.0, 25.0, 30.0]
+SWEEP_ORDERS_E = [16, 64, 256]
+
+
+def sweep_groups(name: str, cfg):
+    """[(config tuple of the group's engine, its SNR points)] of the --sweep of config `name`."""
+    N, M, ch, ratio, eq_name, snr, desc = cfg
+    if name == "d":
+        return [((N, M, ch, ratio, eq_name, q, desc), [q]) for q in SWEEP_SNRS_D]
+    if name == "e":
+        return [((N, m, ch, ratio, eq_name, snr, desc), list(SWEEP_SNRS_E)) for m in SWEEP_ORDERS_E]
+    if M == 0:
+        raise SystemExit("--sweep of an adaptive config other than (d)")
+    return [(cfg, list(SWEEP_GRID))]
+
+
+def measure_sweep(rt: Runtime, args, groups, precision: str, per_gpu: int, factory):
+    """The SNR sweep as the bench step: every step runs all points of every group, `per_gpu`
+    OFDM symbols per GPU each (one complete run per point, new seed per point and step), each
+    group's points pipelined through its engine's LinkEngine.run_pipelined (all groups enqueued
+    before any result is read) and symbol-sharded across ranks; W untimed steps, K timed."""
+    engines = [factory(g, precision) for g, _ in groups]
     total = per_gpu * rt.world
     lanes = args.lanes or 2
-    engine.reserve(total, 2, group=rt.group, lanes=lanes)
-    grid = SWEEP_GRID
+    for eng in engines:
+        eng.reserve(total, 2, group=rt.group, lanes=lanes)
+    npts = sum(len(q) for _, q in groups)
+
+    def one_step(seed_of, events=None, lanes=lanes):
+        pend = []
+        for gi, (eng, (_, snrs)) in enumerate(zip(engines, groups)):
+            pend.append(eng.run_pipelined(total, snrs, [seed_of(gi, k) for k in range(len(snrs))], group=rt.group,
+                                          events=events, lanes=lanes))
+        return [[p.result().bit_errors for p in ps] for ps in pend]
+
     for i in range(args.warmup):
-        for p in engine.run_pipelined(total, grid, [50_000 + 100 * i + k for k in range(len(grid))], group=rt.group,
-                                      lanes=lanes):
-            p.result()
+        one_step(lambda gi, k: 50_000 + 1000 * gi + 100 * i + k)
     rt.sync()
     rt.barrier()
     rt.sync()
     t0 = time.perf_counter()
-    snrs = grid * args.steps
-    seeds = [1000 * st + k for st in range(args.steps) for k in range(len(grid))]
-    pend = engine.run_pipelined(total, snrs, seeds, group=rt.group, lanes=lanes)
-    errs = [p.result().bit_errors for p in pend]
+    # per group one pipelined call over all K steps' points (step-major), every group enqueued
+    # before any count is read back
+    pend = []
+    for gi, (eng, (_, snrs)) in enumerate(zip(engines, groups)):
+        pend.append(eng.run_pipelined(total, snrs * args.steps,
+                                      [1_000_000 * gi + 1000 * st + k for st in range(args.steps)
+                                       for k in range(len(snrs))], group=rt.group, lanes=lanes))
+    errs = [[p.result().bit_errors for p in ps] for ps in pend]
     rt.sync()
     rt.barrier()
     rt.sync()
     elapsed = rt.max_over_ranks(time.perf_counter() - t0)
-    per_point = [sum(errs[k::len(grid)]) for k in range(len(grid))]
-    nbits = engine.valid_bits(total) * args.steps
-    bers = [e / nbits for e in per_point]
     w = PRECISIONS[precision][1]
+    points = []
+    for gi, ((gcfg, snrs), eng) in enumerate(zip(groups, engines)):
+        nbits = eng.valid_bits(total) * args.steps
+        for k, q in enumerate(snrs):
+            e = sum(errs[gi][k::len(snrs)])
+            points.append({"snr_db": q, "qam_order": gcfg[1] if gcfg[1] else "adaptive", "bits_per_ofdm_symbol": eng.bps,
+                           "ber": e / nbits, "bits": nbits})
     # the kernels' launch times for the roofline: one more sweep step after the timed region, on ONE
     # lane with HIP events around every launch -- on two lanes a kernel's events would also span the
-    # other lane's overlapping kernel (round 4's sweep line reported that bound, not a measurement)
-    events = None
+    # other lane's overlapping kernel (round 4's sweep line reported that bound, not a measurement);
+    # the group whose symbols carry the most bits stands for the sweep
+    roof = None
     if not rt.cpu:
+        gi = max(range(len(engines)), key=lambda j: engines[j].bps)
         events = []
-        for p in engine.run_pipelined(total, grid, [90_000 + k for k in range(len(grid))], group=rt.group,
-                                      events=events, lanes=1):
+        for p in engines[gi].run_pipelined(total, groups[gi][1], [90_000 + k for k in range(len(groups[gi][1]))],
+                                           group=rt.group, events=events, lanes=1):
             p.result()
-    roof = roofline(events, N, engine.bps, engine.cp, w, None)
-    if roof is not None:
-        roof["measured"] = ("one untimed sweep step on one HIP stream after the timed region (HIP events "
-                            "around every launch; no overlap between kernels)")
+        roof = roofline(events, groups[gi][0][0], engines[gi].bps, engines[gi].cp, w, None)
+        if roof is not None:
+            roof["measured"] = ("one untimed sweep step of the group with the most bits per symbol, on one HIP stream "
+                                "after the timed region (HIP events around every launch; no overlap between kernels)")
     rec = {
-        "value": total * len(grid) * args.steps / elapsed,
+        "value": total * npts * args.steps / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
         "dtype": PRECISIONS[precision][0],
         "lanes": lanes,
         "roofline": roof,
-        "sweep": {"snr_db": grid, "ber": bers, "bits_per_point": nbits, "points": len(grid),
-                  "symbols_per_point_per_step": total},
+        "sweep": {"snr_db": [pt["snr_db"] for pt in points], "ber": [pt["ber"] for pt in points],
+                  "bits_per_point": points[0]["bits"], "points": npts, "symbols_per_point_per_step": total,
+                  "per_point": points},
     }
-    return engine, rec
+    return engines, rec
 
 
 def main():
@@ -522,8 +564,9 @@ def main():
                     help="clock-ramp warmup before the value_after_ramp measurement (0: skip it)")
     ap.add_argument("--engine-factory", default=None, help=argparse.SUPPRESS)  # tests: module:function
     ap.add_argument("--sweep", action="store_true",
-                    help="one step = the SNR sweep of BASELINE configs[2] (0..30 dB by 1 dB + 26..29 dB by 0.25 dB), "
-                         "--symbols per GPU per point (default 1e5 x 1024/N)")
+                    help="one step = the SNR sweep of BASELINE configs[2] (0..30 dB by 1 dB + 26..29 dB by 0.25 dB); "
+                         "with --config d / e the reference settings' SNR lists of configs[3] / [4] (15/20/25 dB "
+                         "adaptive; 10..30 dB by 5 at 16/64/256-QAM); --symbols per GPU per point (default 1e5 x 1024/N)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="HIP streams the timed runs alternate over (LinkEngine.run_pipelined); default 1, "
                          "--sweep 2 (its 1e5-symbol points overlap a receiver with the next transmitter: "
@@ -604,16 +647,25 @@ def main():
 
 
 def sweep_main(rt: Runtime, args, cfg, factory):
-    """--sweep: the BASELINE configs[2] measurement -- symbols/s over the whole SNR sweep and the
-    BER 1e-4 crossing of the timed runs against the reference-stream path's."""
+    """--sweep: BASELINE configs[2] (config (c), the default) -- symbols/s over the whole SNR sweep and
+    the BER 1e-4 crossing of the timed runs against the reference-stream path's; with --config d / e
+    the reference's own SNR lists of configs[3] / [4] (sweep_groups)."""
     N, M, ch, ratio, eq_name, snr, desc = cfg
-    if M == 0:
-        raise SystemExit("--sweep needs a fixed-order config (b or c)")
+    groups = sweep_groups(args.config, cfg)
     per_gpu = args.symbols if args.symbols else 100_000 // max(1, N // 1024)
-    engine, head = measure_sweep(rt, args, cfg, args.precision, per_gpu, factory)
+    engines, head = measure_sweep(rt, args, groups, args.precision, per_gpu, factory)
+    engine = engines[0]
     total = per_gpu * rt.world
     devices = rt.gather(rt.dev if not rt.cpu else "cpu")
     sw = head["sweep"]
+    if args.config == "d":
+        what = (f"{desc.split(',')[0]} as config/simulation_settings_adaptive.json runs it: SNR 15 / 20 / 25 dB, the "
+                f"bit loading derived per SNR")
+    elif args.config == "e":
+        what = (f"{desc.split(',')[0]} as config/simulation_settings_waterfilling.json runs it: SNR 10..30 dB by 5 at "
+                f"16-, 64- and 256-QAM")
+    else:
+        what = f"{desc.split(',')[0]} as the BASELINE configs[2] SNR sweep: 0..30 dB by 1 dB, 26..29 dB by 0.25 dB"
     out = {
         "metric": "OFDM symbols/sec (1/2/4/8 GPU) at N_FFT=1024 64-QAM; BER ΔdB vs ref",
         "value": head["value"], "unit": "OFDM symbols/s", "n_gpus": rt.world, "devices": devices,
@@ -621,33 +673,40 @@ def sweep_main(rt: Runtime, args, cfg, factory):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": head["dtype"],
         "data": "synthetic: Philox4x32-10 / MWC64X bits and Box-Muller AWGN generated on the GPU per (seed, symbol)",
         "config": {
-            "workload": f"{desc.split(',')[0]} as the BASELINE configs[2] SNR sweep: {sw['points']} points "
-                        f"(0..30 dB by 1 dB, 26..29 dB by 0.25 dB) x {per_gpu} OFDM symbols per GPU per point; "
-                        f"one step = the whole sweep",
-            "n_fft": N, "qam_order": M, "bits_per_ofdm_symbol": engine.bps, "cp": engine.cp, "channel": ch,
-            "equalizer": eq_name, "snr_db": "sweep", "symbols_per_step": total * sw["points"],
-            "parallelism": f"symbol-sharded x{rt.world}",
+            "workload": f"{what}; {sw['points']} points x {per_gpu} OFDM symbols per GPU per point; one step = the "
+                        f"whole sweep",
+            "n_fft": N, "qam_order": SWEEP_ORDERS_E if args.config == "e" else (M if M else "adaptive"),
+            "bits_per_ofdm_symbol": engine.bps if len(engines) == 1 else [e.bps for e in engines],
+            "cp": engine.cp, "channel": ch, "equalizer": eq_name, "snr_db": "sweep",
+            "symbols_per_step": total * sw["points"], "parallelism": f"symbol-sharded x{rt.world}",
         },
         "roofline": head["roofline"],
         "build_id": build_id_or_none(),
         "sweep": sw,
     }
-    c_phx = crossing(sw["snr_db"], sw["ber"])
-    out["ber_1e-4_crossing_db"] = {"throughput": c_phx}
-    if rt.rank == 0 and not args.no_ber_check and not rt.cpu:
-        near = [q for q in sw["snr_db"] if 26.0 <= q <= 29.0]
-        eng64 = make_engine(cfg, "f64")
-        ref = reference_sweep(eng64, N, engine.cp, near, max(1000, args.ref_symbols * 1024 // N))
-        c_ref = crossing(near, ref)
-        out["ber_1e-4_crossing_db"]["reference_streams"] = c_ref
-        out["ber_1e-4_crossing_db"]["reference_symbols_per_point"] = max(1000, args.ref_symbols * 1024 // N)
-        out["ber_1e-4_crossing_db"]["reference_ber"] = dict(zip(near, ref))
-        out["delta_db_at_1e-4"] = None if c_phx is None or c_ref is None else c_phx - c_ref
-        out["bar_db"] = 0.05
+    if args.config == "c" or (args.config not in ("d", "e") and M):
+        c_phx = crossing(sw["snr_db"], sw["ber"])
+        out["ber_1e-4_crossing_db"] = {"throughput": c_phx}
+        if rt.rank == 0 and not args.no_ber_check and not rt.cpu:
+            near = [q for q in sw["snr_db"] if 26.0 <= q <= 29.0]
+            eng64 = make_engine(cfg, "f64")
+            ref = reference_sweep(eng64, N, engine.cp, near, max(1000, args.ref_symbols * 1024 // N))
+            c_ref = crossing(near, ref)
+            out["ber_1e-4_crossing_db"]["reference_streams"] = c_ref
+            out["ber_1e-4_crossing_db"]["reference_symbols_per_point"] = max(1000, args.ref_symbols * 1024 // N)
+            out["ber_1e-4_crossing_db"]["reference_ber"] = dict(zip(near, ref))
+            out["delta_db_at_1e-4"] = None if c_phx is None or c_ref is None else c_phx - c_ref
+            out["bar_db"] = 0.05
+    else:
+        # (d) / (e): no BER 1e-4 crossing inside the reference's SNR list (the adaptive loading holds
+        # SER ~1e-3 at every SNR; 256-QAM stays above 1e-4 to 30 dB) -- the single-point bench lines
+        # carry the BER check of these configs (ber_vs_reference)
+        out["ber_1e-4_crossing_db"] = None
     if rt.rank == 0 and not args.no_cpu_baseline:
-        cpu_cfg = (N, M, ch, ratio, eq_name, 27.75, desc)
+        cpu_cfg = (N, M, ch, ratio, eq_name, 27.75 if args.config == "c" else snr, desc)
         out["cpu_baseline"] = cpu_baseline(cpu_cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
-        out["cpu_baseline"]["sample"] += " (at the sweep's 27.75 dB point: the CPU cost does not depend on the SNR)"
+        out["cpu_baseline"]["sample"] += (" (at one point of the sweep, %s dB: the CPU cost does not depend on the SNR)"
+                                          % cpu_cfg[5])
     if rt.rank == 0:
         print(json.dumps(out), flush=True)
     rt.finish()

@@ -107,3 +107,28 @@ def test_bench_sweep_two_ranks():
     sw = d["sweep"]
     assert sw["points"] == 40 and len(sw["ber"]) == 40 and sw["snr_db"] == bench.SWEEP_GRID
     assert sw["ber"][0] > sw["ber"][-1]  # 0 dB vs 30 dB
+
+
+def test_bench_sweep_config_e_two_ranks():
+    """`bench.py --sweep --config e --gpus 2`: BASELINE configs[4] as config/simulation_settings_waterfilling.json
+    runs it -- SNR 10..30 dB by 5 at 16-, 64- and 256-QAM, one engine per order, every point in one step."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
+                                         os.path.join(ROOT, "ofdm-based-systems_amd"), env.get("PYTHONPATH", "")])
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--engine-factory", "bench_double:make_engine", "--sweep", "--config", "e", "--symbols", "1",
+                        "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-ber-check"],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert d["n_gpus"] == 2 and d["config"]["symbols_per_step"] == 2 * 15
+    assert d["config"]["qam_order"] == [16, 64, 256] and d["config"]["bits_per_ofdm_symbol"] == [4 * 4096, 6 * 4096,
+                                                                                                 8 * 4096]
+    sw = d["sweep"]
+    assert sw["points"] == 15 and sw["snr_db"] == bench.SWEEP_SNRS_E * 3
+    assert [p["qam_order"] for p in sw["per_point"]] == [16] * 5 + [64] * 5 + [256] * 5
+    assert d["ber_1e-4_crossing_db"] is None
