@@ -457,31 +457,10 @@ __device__ __forceinline__ void ds_read16_b64(double (&u)[16], uint32_t la) {
           "i"(o[8]), "i"(o[9]), "i"(o[10]), "i"(o[11]), "i"(o[12]), "i"(o[13]), "i"(o[14]), "i"(o[15])
         : "memory");
 }
-// OFDM_DS_READ16_SPLIT (A/B): the 16 reads as separate statements and their wait as a 17th that the
-// values pass through (round 4's form: the compiler may schedule other work between them)
-#ifndef OFDM_DS_READ16_SPLIT
-#define OFDM_DS_READ16_SPLIT 0
-#endif
-template <int OFF>
-__device__ __forceinline__ void ds_read_b64_at(double& d, uint32_t la) {
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(d) : "v"(la), "i"(OFF) : "memory");
-}
-__device__ __forceinline__ void lgkm_wait16(double (&u)[16]) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]), "+v"(u[7]),
-                   "+v"(u[8]), "+v"(u[9]), "+v"(u[10]), "+v"(u[11]), "+v"(u[12]), "+v"(u[13]), "+v"(u[14]), "+v"(u[15])
-                 :
-                 : "memory");
-}
 // the same with byte offsets Off::at(m), m = 0..15 (Off: a class with a static constexpr at(int))
 template <class Off, int... M>
 __device__ __forceinline__ void ds_read16_b64_seq(double (&u)[16], uint32_t la, std::integer_sequence<int, M...>) {
-    if constexpr (OFDM_DS_READ16_SPLIT) {
-        (ds_read_b64_at<Off::at(M)>(u[M], la), ...);
-        lgkm_wait16(u);
-    } else {
-        ds_read16_b64<Off::at(M)...>(u, la);
-    }
+    ds_read16_b64<Off::at(M)...>(u, la);
 }
 template <class Off>
 __device__ __forceinline__ void ds_read16_b64(double (&u)[16], uint32_t la) {
@@ -1358,12 +1337,10 @@ struct Mwc64x {
 // A workgroup prologue's copy of a global table into LDS, split into load() and store() so that
 // a kernel issues the reads of all its tables before the first wait: each copy loop waited for
 // its own loads (global_load, s_waitcnt vmcnt(0), ds_write per trip), and the prologues of the
-// fused kernels chained five or six memory latencies, ~4 us per workgroup.  The first K trips
+// fused kernels chained five or six memory latencies per workgroup (neutral on the steady state,
+// DESIGN.md section 4, but no longer a chain).  The first K trips
 // of each thread are held in registers; a longer table (MAXN > 8 BLK, or a count not bounded by
 // MAXN: BOUNDED false) copies its remainder in store().  The caller syncs.
-#ifndef OFDM_STAGED_PROLOGUE
-#define OFDM_STAGED_PROLOGUE 1
-#endif
 template <int BLK, int MAXN, typename T, bool BOUNDED = true>
 struct Staged {
     static constexpr int K = MAXN <= 0 ? 0 : ((MAXN + BLK - 1) / BLK < 8 ? (MAXN + BLK - 1) / BLK : 8);

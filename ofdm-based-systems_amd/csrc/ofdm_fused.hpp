@@ -150,16 +150,6 @@ constexpr bool tx_sep_lut() { return sizeof(R) == 8 && FB >= 2 && !(FB & 1) && L
 // VGPR, the element offsets in SGPRs) instead of four 64-bit VGPR addresses (RX b 3.09 -> 3.06,
 // c 3.75 -> 3.70 ms per step at the same occupancy, profiles/r03ab_ab.txt)
 
-// complex128 window-FIR TX (A/B): the outputs stored from the lanes' registers instead of through
-// the row (lane-contiguous: 64 lines per store instruction)
-#ifndef OFDM_FIR_DIRECT_STORE
-#define OFDM_FIR_DIRECT_STORE 0
-#endif
-// complex128 window-FIR TX: the window's LDS reads chained to the samples before them (see k_tx)
-#ifndef OFDM_FIR_STREAM
-#define OFDM_FIR_STREAM 0
-#endif
-
 // MP: multipath channel (L > 1; the generic kernel always takes L from the plan)
 #ifndef OFDM_TX_MP_BLOCK
 #define OFDM_TX_MP_BLOCK 256
@@ -245,33 +235,11 @@ constexpr size_t tx_static_lds() {
 // window FIR (N >= 256, cp <= TPS); -1 any multipath (run-time loop over taps).  ZPW: the complex128
 // window FIR with the zero-padding guard (and its run-time flat path for a one-tap channel) compiled
 // in; without it (cyclic prefix, L > 1: the bench configs) the kernel needs ~139 VGPRs instead of
-// 205-227 and runs 3 waves per SIMD with nothing spilled (with the guard compiled in, 3 waves spilled
-// 39 / 51 dwords at N = 1024 / 2048)
-#ifndef OFDM_F64_FIR_CP3
-#define OFDM_F64_FIR_CP3 0
-#endif
-// workgroup of the 3-wave cyclic-prefix window FIR: at N = 1024 (a symbol per wave) 768 threads keep
-// one copy of the 16 KB per-pass twiddle table for 12 symbols' rows (at 256 threads the table per
-// workgroup caps a CU at two workgroups, 2 waves per SIMD); N = 2048 (two waves per symbol) 768 for
-// the adaptive tables likewise; N = 4096 one symbol per 256-thread workgroup
-#ifndef OFDM_F64_FIR3_BLOCK_10
-#define OFDM_F64_FIR3_BLOCK_10 768
-#endif
-#ifndef OFDM_F64_FIR3_BLOCK_11
-#define OFDM_F64_FIR3_BLOCK_11 768
-#endif
-template <int FB, int LOGN, int LT, bool ZPW>
-constexpr bool f64_fir_cp3() {
-    return OFDM_F64_FIR_CP3 && LT > 0 && !ZPW &&
-           f64_fir_lds(FB, LOGN, LOGN == 10 ? OFDM_F64_FIR3_BLOCK_10 : LOGN == 11 ? OFDM_F64_FIR3_BLOCK_11 : 256,
-                       true) <= 160 * 1024;
-}
+// 205-227 (3 waves per SIMD would fit with nothing spilled; measured no faster)
 template <typename R, int FB, int LOGN, int LT, bool ZPW = false>
 constexpr int tx_block() {
     if (sizeof(R) == 8 && FB > 0) {
         if (LT == 0) return OFDM_F64_TX_BLOCK;
-        if (f64_fir_cp3<FB, LOGN, LT, ZPW>())
-            return LOGN == 10 ? OFDM_F64_FIR3_BLOCK_10 : LOGN == 11 ? OFDM_F64_FIR3_BLOCK_11 : 256;
         return f64_fir_lds(FB, LOGN, OFDM_F64_FIR_BLOCK, LT > 0) <= 160 * 1024 ? OFDM_F64_FIR_BLOCK : 256;
     }
     return FB > 0 && LOGN <= 10 ? (LT != 0 ? OFDM_TX_MP_BLOCK : OFDM_TX_FAST_BLOCK) : kBlock;
@@ -281,7 +249,6 @@ template <typename R, int FB, int LOGN, int LT, bool ZPW = false>
 constexpr int tx_waves() {
     if (sizeof(R) == 8 && FB > 0) {
         if (LT == 0) return OFDM_F64_TX_WAVES;
-        if (f64_fir_cp3<FB, LOGN, LT, ZPW>()) return 3;
         return LOGN >= 12 ? OFDM_F64_FIR_WAVES_4K : OFDM_F64_FIR_WAVES;
     }
     if (FB > 0 && LT > 0 && LOGN > 10) return OFDM_TX_BIG_WFIR_WAVES;
@@ -346,10 +313,6 @@ constexpr int rx_waves() {
 }
 // throughput RX: equaliser coefficients staged in LDS up to N = 2^OFDM_EQ_LDS_MAX_LOGN (beyond,
 // the table would cost a resident workgroup per CU)
-// adaptive RX: the partial-byte path reads the subcarrier table through an opaque pointer (A/B switch)
-#ifndef OFDM_ADAPT_OPAQUE_SC
-#define OFDM_ADAPT_OPAQUE_SC 0
-#endif
 #ifndef OFDM_EQ_LDS_MAX_LOGN
 #define OFDM_EQ_LDS_MAX_LOGN 11
 #endif
@@ -374,10 +337,6 @@ template <typename R, int FB, int LOGN>
 constexpr int rx_grid_rounds() {
     return sizeof(R) == 8 && FB > 0 && LOGN == 10 ? OFDM_RX_GRID_ROUNDS : 0;
 }
-// the complex128 adaptive receiver's MMSE with the four-element batched reciprocal as well (A/B)
-#ifndef OFDM_MMSE_BATCH_ADAPT
-#define OFDM_MMSE_BATCH_ADAPT 1
-#endif
 // the lane's coefficients loaded after the FFT (in flight across the MMSE power reduction)
 template <typename R, int FB, int LOGN, int EQ>
 constexpr bool rx_eq_late() { return f64_rx_solo<R, FB, LOGN>() && EQ > OFDM_EQ_NONE; }
@@ -618,67 +577,48 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
     static_assert(kMaxLuts <= BLK && 32 <= BLK, "one axis entry / tap per thread");
     C hq = mk<R>(0, 0), sep_a = mk<R>(0, 0), sep_b = mk<R>(0, 0), hf = mk<R>(1, 0);
     int ax_off = 0;
-    if (OFDM_STAGED_PROLOGUE) {
-        if constexpr (FOLD_H0) hf = ((const C*)a.h)[0];
-        st_tt.load((const C*)cm.ptw + TTS, TTS);
-        st_lut.load(glut, cm.lut_len);
-        if constexpr (FB == 1) st_sc.load(cm.sc, N);
-        st_ax.load((const Dwords<AxisInfo>*)cm.axis, cm.n_axis);
-        if (threadIdx.x < L && threadIdx.x < 32) hq = ((const C*)a.h)[threadIdx.x];
-        // adaptive: lane l of every wave holds order l's LUT offset, for the codes' lane shuffle
-        if constexpr (FB == 1) {
-            if ((int)(threadIdx.x & 63) < cm.n_axis) ax_off = cm.axis[threadIdx.x & 63].lut_off;
-        }
-        if constexpr (SEP) {
-            if (threadIdx.x < SIDE) sep_a = glut[threadIdx.x], sep_b = glut[threadIdx.x << HB];
-        }
+    if constexpr (FOLD_H0) hf = ((const C*)a.h)[0];
+    st_tt.load((const C*)cm.ptw + TTS, TTS);
+    st_lut.load(glut, cm.lut_len);
+    if constexpr (FB == 1) st_sc.load(cm.sc, N);
+    st_ax.load((const Dwords<AxisInfo>*)cm.axis, cm.n_axis);
+    if (threadIdx.x < L && threadIdx.x < 32) hq = ((const C*)a.h)[threadIdx.x];
+    // adaptive: lane l of every wave holds order l's LUT offset, for the codes' lane shuffle
+    if constexpr (FB == 1) {
+        if ((int)(threadIdx.x & 63) < cm.n_axis) ax_off = cm.axis[threadIdx.x & 63].lut_off;
+    }
+    if constexpr (SEP) {
+        if (threadIdx.x < SIDE) sep_a = glut[threadIdx.x], sep_b = glut[threadIdx.x << HB];
     }
     if constexpr (!TT) load_twiddles<R>(tw, (const C*)cm.tw);
     // the 1/sqrt(N) of ifft(norm="ortho") folded into the LUT (same product per element);
     // flat throughput kernel: the channel tap too (y = h0 ifft(X) = ifft(h0 X)), so the
     // symbol leaves the IFFT as the channel output
     const R lut_scale = scm ? (R)1 : (R)cm.scale;
-    if (OFDM_STAGED_PROLOGUE) {
-        st_tt.store(tt);
-        st_lut.store(lut, [&](const C& v) { return cscale(FOLD_H0 ? cmul(hf, v) : v, lut_scale); });
-        if constexpr (SEP) {
-            // LUT[i] = I[i & (SIDE - 1)] + j Q[i >> HB] exactly (the plan's build_axis verified it):
-            // I from the entries with Q index 0, Q from those with I index 0, the same scaled values
-            if (threadIdx.x < SIDE) {
-                sep_s[threadIdx.x] = sep_a.re * lut_scale;
-                sep_s[SIDE + threadIdx.x] = sep_b.im * lut_scale;
-            }
+    st_tt.store(tt);
+    st_lut.store(lut, [&](const C& v) { return cscale(FOLD_H0 ? cmul(hf, v) : v, lut_scale); });
+    if constexpr (SEP) {
+        // LUT[i] = I[i & (SIDE - 1)] + j Q[i >> HB] exactly (the plan's build_axis verified it):
+        // I from the entries with Q index 0, Q from those with I index 0, the same scaled values
+        if (threadIdx.x < SIDE) {
+            sep_s[threadIdx.x] = sep_a.re * lut_scale;
+            sep_s[SIDE + threadIdx.x] = sep_b.im * lut_scale;
         }
-        st_ax.store((Dwords<AxisInfo>*)axis);
-    } else {
-        for (int i = threadIdx.x; i < TTS; i += BLK) tt[i] = ((const C*)cm.ptw)[TTS + i];
-        if constexpr (FOLD_H0) hf = ((const C*)a.h)[0];
-        for (int i = threadIdx.x; i < cm.lut_len; i += BLK)
-            lut[i] = cscale(FOLD_H0 ? cmul(hf, glut[i]) : glut[i], lut_scale);
-        if constexpr (SEP) {
-            if (threadIdx.x < SIDE) {
-                sep_s[threadIdx.x] = glut[threadIdx.x].re * lut_scale;
-                sep_s[SIDE + threadIdx.x] = glut[threadIdx.x << HB].im * lut_scale;
-            }
-        }
-        if (threadIdx.x < L && threadIdx.x < 32) hq = ((const C*)a.h)[threadIdx.x];
-        if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
     }
+    st_ax.store((Dwords<AxisInfo>*)axis);
     if constexpr (FB == 1) {
         if (threadIdx.x == 0) lut[cm.lut_len] = mk<R>(0, 0);
         auto code = [&](const ScInfo& sc, int off) {
             return sc.lut < 0 ? (uint32_t)cm.lut_len << 8 : ((uint32_t)off << 8) | ((1u << sc.bits) - 1u);
         };
+        // the order's LUT offset from the lane holding it (a dependent global read per element
+        // had been waited for one by one); entries past the staged ones (N > 8 BLK) read directly
         int k0 = threadIdx.x;
-        if (OFDM_STAGED_PROLOGUE) {
-            // the order's LUT offset from the lane holding it (a read per element, dependent on
-            // the staged entry, waited for one by one)
 #pragma unroll
-            for (int q = 0; q < st_sc.K; ++q, k0 += BLK) {
-                const ScInfo sc = st_sc.v[q];
-                const int off = __shfl(ax_off, sc.lut < 0 ? 0 : (int)sc.lut);
-                if (k0 < N) sce[k0] = code(sc, off);
-            }
+        for (int q = 0; q < st_sc.K; ++q, k0 += BLK) {
+            const ScInfo sc = st_sc.v[q];
+            const int off = __shfl(ax_off, sc.lut < 0 ? 0 : (int)sc.lut);
+            if (k0 < N) sce[k0] = code(sc, off);
         }
         for (int k = k0; k < N; k += BLK) {
             const ScInfo sc = cm.sc[k];
@@ -932,12 +872,9 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
                         // (wfir_in(Ah + 8 t + W) = wfir_in(Ah) + 9 t + W + (W + ioff) / 8)
                         constexpr int IOFF = wfir_ioff(LT);
                         R T[8], U[8], V[8];
-                        // the window streamed two samples ahead of its use.  Each read's LDS address
-                        // passes through an empty asm statement that takes the previous sample's
-                        // sum as an input, so the read cannot be issued before that sample arrived:
-                        // left to the compiler (even with a scheduling barrier per sample), all
-                        // 8 + LT - 1 reads were issued at once -- a whole window of 60 live VGPRs at
-                        // the register peak of the kernel
+                        // the window read two samples ahead of its use, in program order (the compiler
+                        // issues all 8 + LT - 1 reads at once either way; tying each read to the previous
+                        // sample's sums through an empty asm ran 1 % slower)
                         typedef const __attribute__((address_space(3))) f64x2* lwin;
                         lwin wl = (lwin)(crow + (wfir_in(Ah, LT) + 9 * to));
                         auto ldw = [&](int k) { const f64x2 u = wl[k]; return mk<R>(u.x, u.y); };
@@ -948,15 +885,6 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
                             const C e = ring[W % 3];
                             const R sw = e.re + e.im;
                             if constexpr (W + 2 < WH) {
-                                if constexpr (OFDM_FIR_STREAM && W > 0) {
-                                    // tied to the previous sample's accumulators (its outputs j in
-                                    // [W - LT, W - 1]): its multiply-adds are issued before this read
-                                    constexpr int j0 = W - LT < 0 ? 0 : W - LT, j1 = W - 1 > 7 ? 7 : W - 1;
-                                    auto jc = [&](int d) -> R { return T[j0 + d <= j1 ? j0 + d : j1]; };
-                                    asm volatile("" : "+v"(wl)
-                                                 : "v"(jc(0)), "v"(jc(1)), "v"(jc(2)), "v"(jc(3)), "v"(jc(4)),
-                                                   "v"(jc(5)), "v"(jc(6)), "v"(jc(7)));
-                                }
                                 ring[(W + 2) % 3] = ldw((W + 2) + ((W + 2 + IOFF) >> 3));
                             }
                             static_for<0, LT>([&](auto Q) {  // tap Q of output j
@@ -975,15 +903,6 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
                             });
                             __builtin_amdgcn_sched_barrier(0);
                         });
-                        if constexpr (OFDM_FIR_STREAM) {
-                            // every accumulator final here, before the branches below (otherwise
-                            // the multiply-adds were sunk past them with the window still live)
-                            asm volatile("" : "+v"(T[0]), "+v"(T[1]), "+v"(T[2]), "+v"(T[3]), "+v"(T[4]), "+v"(T[5]),
-                                              "+v"(T[6]), "+v"(T[7]), "+v"(U[0]), "+v"(U[1]), "+v"(U[2]), "+v"(U[3]),
-                                              "+v"(U[4]), "+v"(U[5]), "+v"(U[6]), "+v"(U[7]));
-                            asm volatile("" : "+v"(V[0]), "+v"(V[1]), "+v"(V[2]), "+v"(V[3]), "+v"(V[4]), "+v"(V[5]),
-                                              "+v"(V[6]), "+v"(V[7]));
-                        }
                         if constexpr (h == 1) {
                             // zero padding: guard output N + t = sum over l > t of h_l x[N + t - l]
                             // (the guard's own samples are zero), stored and counted
@@ -1017,20 +936,6 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
                                 pys = __builtin_fma(pr, pr, pys);
                                 pys = __builtin_fma(pi, pi, pys);
                             }
-                        }
-                        if constexpr (OFDM_FIR_DIRECT_STORE && TPS >= 64) {
-                            // (A/B) the lane's 8 consecutive outputs stored from the registers: 8 store
-                            // instructions of 64 distinct 128-byte lines each, no LDS transpose
-                            C* yh = yout + sl * ystride + h * NH;
-                            gptr<C> yg = lane_ptr(uniform_ptr(yh), (uint32_t)(8 * to));
-#pragma unroll
-                            for (int j = 0; j < 8; ++j) {
-                                const C yv = mk<R>(T[j] - U[j], T[j] + V[j]);
-                                pys = __builtin_fma(yv.re, yv.re, pys);
-                                pys = __builtin_fma(yv.im, yv.im, pys);
-                                if (store) st_stream<false>(yg + j, yv);
-                            }
-                            return;
                         }
                         sym_sync<TPS>();  // every window is read: the outputs take the row
 #pragma unroll
@@ -1270,18 +1175,16 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     constexpr bool EQ_PRE =
         !EQ_LDS && !EQ_LATE && ((FB > 0 && EQ > OFDM_EQ_NONE) || (FB == 0 && sizeof(R) == 4));
     constexpr bool EQ_REG = EQ_PRE || EQ_LATE;  // coefficients in registers (ecoef)
-    constexpr bool MMSE_BATCH = sizeof(R) == 8 && FB > 0 && EQ == OFDM_EQ_MMSE && OFDM_MMSE_BATCH_ADAPT >= (FB == 1);
+    constexpr bool MMSE_BATCH = sizeof(R) == 8 && FB > 0 && EQ == OFDM_EQ_MMSE;
 
     // the tables' global reads issued first (Staged), the noise table built while they fly
     Staged<BLK, (FB > 1 && MV ? 2 : 1) * TTS, C> st_tt;
     Staged<BLK, EQ_LDS ? N : 0, C> st_eq;
     Staged<BLK, kMaxLuts, Dwords<AxisInfo>> st_ax;
     static_assert(kMaxLuts <= BLK, "one axis entry per thread");
-    if (OFDM_STAGED_PROLOGUE) {
-        st_tt.load((const C*)cm.ptw, tts_all);
-        if constexpr (EQ_LDS) st_eq.load((const C*)cm.eq_a, N);
-        st_ax.load((const Dwords<AxisInfo>*)cm.axis, cm.n_axis);
-    }
+    st_tt.load((const C*)cm.ptw, tts_all);
+    if constexpr (EQ_LDS) st_eq.load((const C*)cm.eq_a, N);
+    st_ax.load((const Dwords<AxisInfo>*)cm.axis, cm.n_axis);
     // sigma from the whole-stream mean power (noise/models.py:13-22)
     const bool noise = a.noise_on && !(flags & 1);
     double sigma_d = 0;
@@ -1292,21 +1195,14 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     const R sigma = (R)sigma_d;
     build_noise_table(ntab, sigma_d, ntab64);
     if constexpr (!TT) load_twiddles<R>(tw, (const C*)cm.tw);
-    if (OFDM_STAGED_PROLOGUE) {
-        st_tt.store(tt);
-        if constexpr (EQ_LDS) st_eq.store(eqt);
-        st_ax.store((Dwords<AxisInfo>*)axis);
-    } else {
-        for (int i = threadIdx.x; i < tts_all; i += BLK) tt[i] = ((const C*)cm.ptw)[i];
-        if constexpr (EQ_LDS)
-            for (int k = threadIdx.x; k < N; k += BLK) eqt[k] = ((const C*)cm.eq_a)[k];
-        if (threadIdx.x < cm.n_axis) axis[threadIdx.x] = cm.axis[threadIdx.x];
-    }
+    st_tt.store(tt);
+    if constexpr (EQ_LDS) st_eq.store(eqt);
+    st_ax.store((Dwords<AxisInfo>*)axis);
     if constexpr (FB == 1 && sizeof(R) == 8) {
         if (threadIdx.x < 8) {
             OrderParams64 o = OrderParams64::make(0.0, 0.0, 0.0, 0u);  // unused subcarrier: level 0, no bits
             if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
-                const AxisInfo ax = OFDM_STAGED_PROLOGUE ? __builtin_bit_cast(AxisInfo, st_ax.v[0]) : cm.axis[threadIdx.x];
+                const AxisInfo ax = __builtin_bit_cast(AxisInfo, st_ax.v[0]);  // (thread < n_axis <= kMaxLuts)
                 const double span = (double)(ax.side - 1);
                 o = OrderParams64::make(ax.inv_step * cm.scale / span,  // mul: the FFT output stays unscaled
                                         ax.lev0 * ax.inv_step / span,   // add: negated in the FMA
@@ -1319,7 +1215,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
             // unused subcarrier: level 0, no bits
             OrderParams o{0.f, 0.f, 0u, 0u};
             if (threadIdx.x < cm.n_axis && threadIdx.x != kUnusedOrder) {
-                const AxisInfo ax = OFDM_STAGED_PROLOGUE ? __builtin_bit_cast(AxisInfo, st_ax.v[0]) : cm.axis[threadIdx.x];
+                const AxisInfo ax = __builtin_bit_cast(AxisInfo, st_ax.v[0]);  // (thread < n_axis <= kMaxLuts)
                 const double span = (double)(ax.side - 1);  // see OrderParams
                 o.mul = (float)(ax.inv_step * cm.scale / span);  // the FFT output stays unscaled
                 o.add = (float)(-ax.lev0 * ax.inv_step / span);
@@ -1603,13 +1499,8 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                     if (!all_valid) {
                         // a trailing partial byte of the run is not compared (constellation/
                         // adaptive.py:259-263): keep the first bits (MSB first) of the valid range.
-                        // (The table is read through an opaque pointer: otherwise the compiler
-                        // reuses the launch-invariant reads of the order codes above and keeps all
-                        // 16 entries -- or their addresses -- in registers through the symbol loop,
-                        // for a branch only the run's last symbol takes.)
                         static_assert(sizeof(ScInfo) == 8, "ScInfo is one 8-byte word");
                         gptr<const uint64_t> scp = (gptr<const uint64_t>)cm.sc;
-                        if (OFDM_ADAPT_OPAQUE_SC) asm volatile("" : "+s"(scp));
                         uint32_t vm = 0;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
