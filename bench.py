@@ -547,7 +547,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps before the K timed ones (default 10, ~0.1 s of config (b): past the "
+                         "first launches' code-object loads, workspace allocations and the clock's first transient)")
     ap.add_argument("--symbols", type=int, default=0,
                     help="OFDM symbols per GPU per step (default 1e6 x 1024/N)")
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
