@@ -947,6 +947,13 @@ struct PermSlicer64 {
         asm("v_fma_f64 %0, %1, %2, %3" : "=v"(f) : "v"(v), "v"(smax), "s"(magic));
         return (uint32_t)__builtin_bit_cast(uint64_t, f);
     }
+    // the same with a per-element level multiplier m = s mul (z s the point: the MMSE scale s folded in)
+    __device__ __forceinline__ uint32_t level_m(double u, double m) const {
+        double v, f;
+        asm("v_fma_f64 %0, %1, %2, -%3 clamp" : "=v"(v) : "v"(u), "v"(m), "v"(add));
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(f) : "v"(v), "v"(smax), "s"(magic));
+        return (uint32_t)__builtin_bit_cast(uint64_t, f);
+    }
     __device__ __forceinline__ uint32_t diff(const cpx<double> (&z)[4], uint32_t txw) const {
         uint32_t li[4], lq[4];
 #pragma unroll
@@ -954,6 +961,19 @@ struct PermSlicer64 {
             li[j] = level(z[j].re);
             lq[j] = level(z[j].im);
         }
+        return combine(li, lq, txw);
+    }
+    __device__ __forceinline__ uint32_t diff_scaled(const cpx<double> (&z)[4], const double (&s)[4], uint32_t txw) const {
+        uint32_t li[4], lq[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double m = s[j] * mul;
+            li[j] = level_m(z[j].re, m);
+            lq[j] = level_m(z[j].im, m);
+        }
+        return combine(li, lq, txw);
+    }
+    __device__ __forceinline__ uint32_t combine(const uint32_t (&li)[4], const uint32_t (&lq)[4], uint32_t txw) const {
         const uint32_t si = __builtin_amdgcn_perm(__builtin_amdgcn_perm(li[3], li[2], 0x0c0c0400u),
                                                   __builtin_amdgcn_perm(li[1], li[0], 0x0c0c0400u), 0x05040100u);
         const uint32_t sq = __builtin_amdgcn_perm(__builtin_amdgcn_perm(lq[3], lq[2], 0x0c0c0400u),
@@ -1102,17 +1122,19 @@ struct alignas(16) OrderParams64 {
     }
 };
 static_assert(sizeof(OrderParams64) == 32, "two 16-byte halves");
-template <bool SMALL>
+// SCALED: z unscaled and s[j] its MMSE scale, folded into the order's level multiplier
+template <bool SMALL, bool SCALED = false>
 __device__ __forceinline__ uint32_t adaptive_diff64(const cpx<double> (&z)[4], const OrderParams64* const (&op)[4],
-                                                    uint32_t txw, double magic) {
+                                                    uint32_t txw, double magic, const double (&s)[4]) {
     uint32_t li[4], lq[4], meta[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const f64x2 ma = op[j]->ma;  // {mul, add}
         const f64x2 sm = op[j]->sm;  // {smax, meta}
+        const double m = SCALED ? s[j] * ma.x : ma.x;
         double vi, vq, fi, fq;
-        asm("v_fma_f64 %0, %1, %2, -%3 clamp" : "=v"(vi) : "v"(z[j].re), "v"(ma.x), "v"(ma.y));
-        asm("v_fma_f64 %0, -%1, %2, -%3 clamp" : "=v"(vq) : "v"(z[j].im), "v"(ma.x), "v"(ma.y));
+        asm("v_fma_f64 %0, %1, %2, -%3 clamp" : "=v"(vi) : "v"(z[j].re), "v"(m), "v"(ma.y));
+        asm("v_fma_f64 %0, -%1, %2, -%3 clamp" : "=v"(vq) : "v"(z[j].im), "v"(m), "v"(ma.y));
         asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fi) : "v"(vi), "v"(sm.x), "s"(magic));
         asm("v_fma_f64 %0, %1, %2, %3" : "=v"(fq) : "v"(vq), "v"(sm.x), "s"(magic));
         li[j] = (uint32_t)__builtin_bit_cast(uint64_t, fi);

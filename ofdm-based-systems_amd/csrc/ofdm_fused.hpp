@@ -1445,7 +1445,9 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
             };
             // MMSE in complex128: conj(H) v / (|H|^2 + nv) of a lane word's four elements, the four
             // reciprocals from one (MMSE_BATCH)
-            auto mmse4 = [&](int q, C(&z)[4]) {
+            // (sc non-null: z = conj(H) v unscaled and sc[j] = 1 / (|H|^2 + nv), the slicer folding the
+            // scale into its level multiplier: one product per element instead of two)
+            auto mmse4 = [&](int q, C(&z)[4], R* sc) {
                 C c[4];
                 R dn[4], inv[4];
 #pragma unroll
@@ -1467,7 +1469,14 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                     for (int j = 0; j < 4; ++j) inv[j] = recip<R>(dn[j]);
                 }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) z[j] = cscale(cmul(x[4 * q + j], c[j]), inv[j]);
+                for (int j = 0; j < 4; ++j) {
+                    if (sc) {
+                        z[j] = cmul(x[4 * q + j], c[j]);
+                        sc[j] = inv[j];
+                    } else {
+                        z[j] = cscale(cmul(x[4 * q + j], c[j]), inv[j]);
+                    }
+                }
             };
             if constexpr (FB == 1) {
                 // four elements per lane word, each through its subcarrier's order (the codes
@@ -1479,8 +1488,9 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                     const OP* op[4];
                     uint32_t oc = ocode[q];
                     asm volatile("" : "+v"(oc));
+                    R sc[4] = {1, 1, 1, 1};  // the MMSE scale per element, folded into the slicer
                     if (MMSE_BATCH) {
-                        mmse4(q, z);
+                        mmse4(q, z, sc);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
@@ -1490,8 +1500,8 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                         op[j] = (const OP*)((const unsigned char*)ordt + ((oc >> (8 * j)) & 0xFFu));
                     uint32_t d;
                     if constexpr (sizeof(R) == 8)
-                        d = small_orders ? adaptive_diff64<true>(z, op, lane_word(tb.lane, q), magic64)
-                                         : adaptive_diff64<false>(z, op, lane_word(tb.lane, q), magic64);
+                        d = small_orders ? adaptive_diff64<true, MMSE_BATCH>(z, op, lane_word(tb.lane, q), magic64, sc)
+                                         : adaptive_diff64<false, MMSE_BATCH>(z, op, lane_word(tb.lane, q), magic64, sc);
                     else
                         d = small_orders ? adaptive_diff<true>(z, op, lane_word(tb.lane, q))
                                          : adaptive_diff<false>(z, op, lane_word(tb.lane, q));
@@ -1522,8 +1532,10 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                         if (!scm) load_coef4(q + 1);  // (single carrier: loaded before its equaliser)
                     }
                     C z[4];
-                    if (MMSE_BATCH && !scm) {
-                        mmse4(q, z);
+                    R sc[4];  // MMSE_BATCH: the scale per element, folded into the QAM slicer
+                    const bool fold = MMSE_BATCH && !scm;
+                    if (fold) {
+                        mmse4(q, z, sc);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j) z[j] = equalized(4 * q + j);
@@ -1535,10 +1547,14 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                     if (FB_PSK_ONLY || (FB <= 4 && cm.psk_m > 0)) {
                         uint32_t r = 0;
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) r |= psk_decide(z[j], cm) << (8 * j);
+                        for (int j = 0; j < 4; ++j) r |= psk_decide(fold ? cscale(z[j], sc[j]) : z[j], cm) << (8 * j);
                         d = r ^ (lane_word(tb.lane, q) & PermSlicer<FB>::BYTE_MASK);
                     } else if constexpr (!FB_PSK_ONLY) {
-                        d = pslicer.diff(z, lane_word(tb.lane, q));
+                        if constexpr (MMSE_BATCH) {
+                            d = fold ? pslicer.diff_scaled(z, sc, lane_word(tb.lane, q)) : pslicer.diff(z, lane_word(tb.lane, q));
+                        } else {
+                            d = pslicer.diff(z, lane_word(tb.lane, q));
+                        }
                     }
                     bes += __popc(d);
                     ses += PermSlicer<FB>::nonzero_bytes(d);
