@@ -482,15 +482,13 @@ def measure_sweep(rt: Runtime, args, groups, precision: str, per_gpu: int, facto
         eng.reserve(total, 2, group=rt.group, lanes=lanes)
     npts = sum(len(q) for _, q in groups)
 
-    def one_step(seed_of, events=None, lanes=lanes):
-        pend = []
-        for gi, (eng, (_, snrs)) in enumerate(zip(engines, groups)):
-            pend.append(eng.run_pipelined(total, snrs, [seed_of(gi, k) for k in range(len(snrs))], group=rt.group,
-                                          events=events, lanes=lanes))
-        return [[p.result().bit_errors for p in ps] for ps in pend]
-
-    for i in range(args.warmup):
-        one_step(lambda gi, k: 50_000 + 1000 * gi + 100 * i + k)
+    for i in range(args.warmup):  # one untimed sweep per warmup step, every group enqueued first
+        pend = [eng.run_pipelined(total, snrs, [50_000 + 1000 * gi + 100 * i + k for k in range(len(snrs))],
+                                  group=rt.group, lanes=lanes)
+                for gi, (eng, (_, snrs)) in enumerate(zip(engines, groups))]
+        for ps in pend:
+            for p in ps:
+                p.result()
     rt.sync()
     rt.barrier()
     rt.sync()
