@@ -246,6 +246,24 @@ def pmc_traffic(key: str, symbols_per_launch: int):
     return {k: v * symbols_per_launch / rec["symbols_per_launch"] for k, v in rec["bytes_per_launch"].items()}
 
 
+def pmc_issue(key: str):
+    """Issue fractions of the fused kernels from committed rocprofv3 SQ counters
+    (profiles/pmc_summary.json[key]['issue'], tools/pmc_summary.py --counters), or None when they
+    were measured on other kernel sources."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f).get(key, {}).get("issue")
+    if not rec:
+        return None
+    from ofdm_based_systems import _backend as B
+
+    if rec.get("build_id") != B.build_id():
+        return None
+    return rec
+
+
 def build_id_or_none():
     try:
         from ofdm_based_systems import _backend as B
@@ -351,9 +369,14 @@ def timed_steps(rt: Runtime, engine, total: int, snr: float, steps: int, seed0: 
     return rt.max_over_ranks(time.perf_counter() - t0), bit_errors
 
 
-def roofline(events, N: int, bps: int, cp: int, w: int, traffic):
+def roofline(events, N: int, bps: int, cp: int, w: int, traffic, issue=None):
     """The dominant kernel's algorithmic bytes per launch over its average launch time (HIP
-    events recorded on the launch stream around every ofdm_tx / ofdm_rx)."""
+    events recorded on the launch stream around every ofdm_tx / ofdm_rx).
+
+    issue (pmc_issue): the committed SQ counters of this build -- then roofline.issue carries the
+    dominant kernel's VALU / LDS issue fractions of the SIMDs' time, and `bound` names whichever
+    ceiling is closer: "hbm" (achieved / peak, the HBM fraction) or "valu" (the SIMDs' VALU issue
+    fraction).  achieved / peak / frac stay the HBM figures either way."""
     if not events:
         return None
     durs = {}
@@ -364,13 +387,27 @@ def roofline(events, N: int, bps: int, cp: int, w: int, traffic):
     per_launch = durs[dom][0][1]
     alg = kernel_bytes_per_symbol(N, bps, cp, w)
     achieved = alg * per_launch / avg[dom] / 1e9
-    return {
+    out = {
         "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS,
         "traffic": None if traffic is None else traffic.get(dom),
         "alg_bytes_per_symbol": alg, "symbols_per_launch": per_launch,
         "avg_launch_ms": {k: v * 1e3 for k, v in avg.items()},
     }
+    kd = (issue or {}).get("kernels", {})
+    if dom in kd:
+        k = kd[dom]
+        out["issue"] = {
+            "valu": k.get("valu"), "lds": k.get("lds"), "any": k.get("any"),
+            "waves_per_simd": k.get("waves_per_simd"),
+            "valu_insts_per_symbol": k.get("per_symbol", {}).get("SQ_INSTS_VALU"),
+            "other_kernel": {n: {"valu": v.get("valu"), "lds": v.get("lds")} for n, v in kd.items() if n != dom},
+            "source": f"profiles/{issue['tag']}_issue.json (rocprofv3 SQ counters of build {issue['build_id']}; "
+                      "fraction of the SIMDs' time issuing, GRBM_GUI_ACTIVE as the kernel's duration)",
+        }
+        if (k.get("valu") or 0.0) > out["frac"]:
+            out["bound"] = "valu"
+    return out
 
 
 def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp: bool):
@@ -394,7 +431,8 @@ def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp:
         "value": total * args.steps / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
         "dtype": PRECISIONS[precision][0],
-        "roofline": roofline(events, N, bps, cp, w, None if rt.cpu else pmc_traffic(key, per_gpu)),
+        "roofline": roofline(events, N, bps, cp, w, None if rt.cpu else pmc_traffic(key, per_gpu),
+                             None if rt.cpu else pmc_issue(key)),
         "ber": bit_errors / (engine.valid_bits(total) * args.steps),
         "bits": engine.valid_bits(total) * args.steps,
     }
@@ -535,7 +573,11 @@ def measure_sweep(rt: Runtime, args, groups, precision: str, per_gpu: int, facto
         "lanes": lanes,
         "roofline": roof,
         "sweep": {"snr_db": [pt["snr_db"] for pt in points], "ber": [pt["ber"] for pt in points],
-                  "bits_per_point": points[0]["bits"], "points": npts, "symbols_per_point_per_step": total,
+                  # one value when every group's symbols carry the same bits, else one per group (in
+                  # group order; per_point[*].bits holds every point's own)
+                  "bits_per_point": (points[0]["bits"] if len({pt["bits"] for pt in points}) == 1
+                                     else [eng.valid_bits(total) * args.steps for eng in engines]),
+                  "points": npts, "symbols_per_point_per_step": total,
                   "per_point": points},
     }
     return engines, rec
@@ -615,8 +657,9 @@ def main():
         "vs_baseline": None,
         "dtype": head["dtype"],
         "data": "synthetic: Philox4x32-10 / MWC64X bits and Box-Muller AWGN (64-point phase table) generated "
-                "on the GPU per (seed, symbol); noise radius exact to 5.65 sigma (BER curves valid down to "
-                "~1e-7)",
+                "on the GPU per (seed, symbol), stream version 3: the noise radius is the Rayleigh quantile at "
+                "the midpoints of 2^31 equiprobable cells (its tail exact at every cell boundary down to "
+                "6.555 sigma), the component tail within 2^-33 of the Gaussian",
         "config": {
             "workload": f"{desc}; {per_gpu} OFDM symbols per GPU per step",
             "n_fft": N, "qam_order": M if M else "adaptive", "bits_per_ofdm_symbol": engine.bps, "cp": engine.cp,
@@ -705,8 +748,15 @@ def sweep_main(rt: Runtime, args, cfg, factory):
     if rt.rank == 0 and not args.no_cpu_baseline:
         cpu_cfg = (N, M, ch, ratio, eq_name, 27.75 if args.config == "c" else snr, desc)
         out["cpu_baseline"] = cpu_baseline(cpu_cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
-        out["cpu_baseline"]["sample"] += (" (at one point of the sweep, %s dB: the CPU cost does not depend on the SNR)"
-                                          % cpu_cfg[5])
+        if args.config == "e":
+            out["cpu_baseline"]["sample"] += (" (the 256-QAM group's engine only, at %s dB -- the sweep's other groups are "
+                                              "16- and 64-QAM, whose CPU cost per symbol is lower)" % cpu_cfg[5])
+        elif args.config == "d":
+            out["cpu_baseline"]["sample"] += (" (the %s dB point's bit loading only: every point of the sweep has its "
+                                              "own plan)" % cpu_cfg[5])
+        else:
+            out["cpu_baseline"]["sample"] += (" (at one point of the sweep, %s dB: the CPU cost does not depend on the "
+                                              "SNR)" % cpu_cfg[5])
     if rt.rank == 0:
         print(json.dumps(out), flush=True)
     rt.finish()

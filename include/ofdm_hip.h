@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define OFDM_ABI_VERSION 4
+#define OFDM_ABI_VERSION 5
 
 #define OFDM_OK 0
 #define OFDM_E_INVALID (-1)  /* bad argument / unsupported shape          */
@@ -159,7 +159,8 @@ int ofdm_demap_count(ofdm_plan_t plan, void* stream, const void* Z, const uint8_
 int ofdm_nn_classify(void* stream, const double* lut, int32_t m, const void* z, int64_t n,
                      int64_t* idx);
 
-/* Throughput-mode noise radius (ABI 4): radius[i] = sqrt(32 - log2(float(words[i] | 0x1F8))),
+/* Throughput-mode noise radius (ABI 4; ABI 5: stream version 3, the radius takes the whole word):
+   radius[i] = sqrt(32 - log2(float(words[i] | 1))),
    evaluated exactly as the fused receivers evaluate it for every lane word (the float32 hardware
    log2 / square root: the one step of the stream definition, csrc/ofdm_device.hpp noise_radius,
    that IEEE arithmetic does not pin).  AWGNoiseModel.add_noise's Gaussian (noise/models.py:19-21)
@@ -203,9 +204,11 @@ int ofdm_power(ofdm_plan_t plan, void* stream, const void* y, int64_t len, doubl
  * Bit source: `bits` != NULL -> packed tx bytes of the WHOLE run (OFDM symbol s
  * starts at bit s*bits_per_ofdm_symbol), e.g. the reference's PCG64 bytes
  * (parity mode).  bits == NULL -> throughput mode: bits and noise from the
- * counter-based lane streams keyed by (seed, global symbol) (stream version 2:
+ * counter-based lane streams keyed by (seed, global symbol) (stream version 3 since ABI 5:
  * Philox4x32-10 seeding MWC64X; definition in csrc/ofdm_device.hpp, restated in
- * oracle/philox_streams.py).  n_sym = 0 is an empty call (returns 0, launches nothing).
+ * oracle/philox_streams.py).  Caller bits on the bench shapes (complex128 OFDM, cyclic prefix,
+ * 64-QAM at N = 1024 or 256-QAM at N = 4096) run the throughput kernels with the bit -- and in
+ * ofdm_rx, with nr/ni and no z_out, the noise -- source swapped; other shapes the generic kernel.  n_sym = 0 is an empty call (returns 0, launches nothing).
  *
  * ofdm_tx: for global OFDM symbols [sym0, sym0+n_sym): map -> IFFT(ortho) (OFDM) or
  *   nothing (single carrier) -> cyclic prefix or zero guard -> linear convolution with

@@ -30,9 +30,15 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 
+// (kNotInBuild: a dispatch that reached a shape an OFDM_AB_ONLY experiment build does not
+// instantiate -- reported as a bad argument naming the build, not as a HIP error)
 #define HIPCHK(expr)                                                                       \
     do {                                                                                   \
         hipError_t _e = (expr);                                                            \
+        if (kAbOnly && _e == kNotInBuild)                                                  \
+            return fail(OFDM_E_INVALID, std::string(#expr ": kernel not in this build (an "  \
+                                                    "OFDM_AB_ONLY variant instantiates "     \
+                                                    "N = 1024..4096 only)"));               \
         if (_e != hipSuccess)                                                              \
             return fail(OFDM_E_HIP, std::string(#expr ": ") + hipGetErrorString(_e));      \
     } while (0)

@@ -1248,14 +1248,22 @@ __device__ __forceinline__ u4 philox4x32_10(u4 c, uint32_t k0, uint32_t k1) {
 }
 
 // ------------------------------------------------------------------ throughput-mode streams
-// Definition (philox mode, stream version 2): thread t of OFDM symbol s owns elements
+// Definition (philox mode, stream version 3): thread t of OFDM symbol s owns elements
 // k = t + TPS*i.  One Philox4x32-10 block per lane, key = seed, counter = (t, s mod 2^32,
 // s >> 32, kLane), gives words P0..P3.  The lane's 128 payload bits are the words
 // (P2, P3, m0, m1) (element i takes the low b_k bits of byte i, see lane_bits), where m0, m1,
-// ... are the outputs of an MWC64X generator seeded with x = P0, c = (P1 >> 1) | 1.  Output
-// m(2 + i) is the complex noise of element i (Mwc64x::noise): the radius from the word with
-// bits 3..8 set, the phase from bits 3..8 through a 64-entry table.  Everything depends only
-// on (seed, s, N), so results do not depend on how symbols are batched or sharded.
+// ... are the outputs of an MWC64X generator seeded with x = P0, c = (P1 >> 1) | 1.  The
+// generator then continues into the lane's noise samples j = 0, 1, ... (the E elements, then
+// the zero-padding tail samples it owns): before samples j = 0, 4, 8, ... it draws a phase
+// word q, and every sample draws its radius word w (Mwc64x::draw) -- outputs m2 = q0,
+// m3..m6 = w0..w3, m7 = q1, ...  Sample j's complex normal is radius(w) times phase-table
+// entry (q >> 8 (j & 3)) & 63 (Mwc64x::add_noise).  Everything depends only on (seed, s, N),
+// so results do not depend on how symbols are batched or sharded.
+// (Stream version 2 took the phase from bits 3..8 of the radius word and forced them to one
+// in the radius, which truncated the radius at 5.65 sigma; version 3 gives the radius the whole
+// word -- the Rayleigh quantile at the midpoints of 2^31 equiprobable cells, exact at every cell
+// boundary down to P = 2^-31 at 6.555 sigma -- and costs one generator step per four samples,
+// where version 2 recomputed x ^ c for each phase.)
 constexpr uint32_t kLane = 0x1A7E5EEDu;
 
 __device__ __forceinline__ u4 philox_lane(uint64_t seed, int64_t s, uint32_t t, uint32_t stream) {
@@ -1278,13 +1286,11 @@ __device__ __forceinline__ uint32_t lane_bits(const u4& w, int i, int b) {
 }
 
 // Noise phase table: kNoisePhases points e^{2 pi i (j + 1/2) / 64} scaled by
-// sigma sqrt(2 ln 2) (float32), one per workgroup in LDS; entry j lives at byte 8 j, so a
-// word's bits 3..8 are its byte offset.  A uniform phase taken on 64 points leaves the
-// noise's projection on any direction Gaussian to within the trapezoid rule's error on
-// the smooth periodic tail integrand: P(Re(n e^{-i phi}) > d sigma) is off by < 2e-6 relative
-// for every phi and d >= 1, < 1e-10 at d >= 3 (tests/test_oracle_philox.py).
+// sigma sqrt(2 ln 2) (float32), one per workgroup in static LDS.  A uniform phase taken on 64
+// points leaves the noise's projection on any direction Gaussian to within the trapezoid rule's
+// error on the smooth periodic tail integrand: P(Re(n e^{-i phi}) > d sigma) is off by < 2e-6
+// relative for every phi and d >= 1, < 1e-10 at d >= 3 (tests/test_oracle_philox.py).
 constexpr int kNoisePhases = 64;
-constexpr uint32_t kNoisePhaseMask = 0x1F8u;      // bits 3..8: byte offset of entry j
 constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2)
 
 // MWC64X (D. B. Thomas, multiply-with-carry, base 2^32, A = 4294883355): state (x, c),
@@ -1292,15 +1298,19 @@ constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2)
 // carry into the addend pair and the xor) per 32-bit output.  Seeded from one Philox block:
 // c = (P1 >> 1) | 1 < A, so the state is never one of the two fixed points.
 constexpr uint32_t kMwcA = 4294883355u;
-// sqrt(32 - log2(float(w | 0x1F8))) on the float32 hardware log2 / sqrt.  The |.| (a free source
-// modifier) keeps the square root real when the approximate log2 of a word rounding to 2^32
-// comes out slightly above 32: the radius is then ~0 instead of NaN.
+// sqrt(32 - log2(float(w | 1))) on the float32 hardware log2 / sqrt: sigma sqrt(-2 ln u) / (sigma
+// sqrt(2 ln 2)) with u = float(w | 1) 2^-32 in [2^-32, 1] (words 2k and 2k + 1 share the cell
+// midpoint (2k + 1) 2^-32, so u > 0; the largest radius is sqrt(32) sqrt(2 ln 2) = 6.660 sigma, the
+// next 6.493).  The |.| (a free source
+// modifier) keeps the square root real when the approximate log2 of a word rounding to 2^32 comes
+// out slightly above 32: the radius is then ~0 instead of NaN.
 __device__ __forceinline__ float noise_radius(uint32_t w) {
-    return __builtin_amdgcn_sqrtf(__builtin_fabsf(32.0f - __builtin_amdgcn_logf((float)(w | kNoisePhaseMask))));
+    return __builtin_amdgcn_sqrtf(__builtin_fabsf(32.0f - __builtin_amdgcn_logf((float)(w | 1u))));
 }
 
 struct Mwc64x {
     uint32_t x, c;
+    uint32_t q;  // the current phase word (noise samples 4 (j >> 2) .. 4 (j >> 2) + 3)
     __device__ __forceinline__ void seed(uint32_t p0, uint32_t p1) {
         x = p0;
         c = (p1 >> 1) | 1u;
@@ -1312,44 +1322,50 @@ struct Mwc64x {
         c = (uint32_t)(v >> 32);
         return r;
     }
-    // One complex normal with per-component standard deviation sigma added to x, from one
-    // output w by Box-Muller: u = float(w | 0x1F8) 2^-32 in (1.2e-7, 1] (the radius tail is
-    // exact to 5.6 sigma), radius sigma sqrt(-2 ln u) = sigma sqrt(2 ln 2) sqrt(32 - log2(w | 0x1F8))
-    // on the hardware v_log_f32 (log2) / v_sqrt_f32, phase from bits 3..8 through ntab (already
-    // holding sigma sqrt(2 ln 2)).  Bits 3..8 are forced to 1 in the radius word, so radius and
-    // phase come from disjoint bits.
-    __device__ __forceinline__ static f32x2 sample(uint32_t w, const f32x2* ntab, float& r) {
-        r = noise_radius(w);
-        return *(const f32x2*)((const unsigned char*)ntab + (w & kNoisePhaseMask));
+    // noise sample j of the lane (j a compile-time constant in the unrolled kernels): the phase
+    // word first when j = 0 mod 4, then the sample's radius word
+    __device__ __forceinline__ uint32_t draw(int j) {
+        if ((j & 3) == 0) q = next();
+        return next();
     }
-    __device__ __forceinline__ void add_noise(f32x2& x0, const f32x2* ntab) {
+    // byte offset of sample j's phase entry in a table of ENTRY-byte entries
+    template <int ENTRY>
+    __device__ __forceinline__ uint32_t phase_off(int j) const {
+        return ((q >> (8 * (j & 3))) & (uint32_t)(kNoisePhases - 1)) * (uint32_t)ENTRY;
+    }
+    // One complex normal with per-component standard deviation sigma, noise sample j: radius
+    // sigma sqrt(-2 ln u) = sigma sqrt(2 ln 2) sqrt(32 - log2(w | 1)) on the hardware v_log_f32
+    // (log2) / v_sqrt_f32, the phase entry (already holding sigma sqrt(2 ln 2)) from the phase word.
+    __device__ __forceinline__ f32x2 sample(int j, const f32x2* ntab, float& r) {
+        r = noise_radius(draw(j));
+        return *(const f32x2*)((const unsigned char*)ntab + phase_off<sizeof(f32x2)>(j));
+    }
+    __device__ __forceinline__ void add_noise(f32x2& x0, const f32x2* ntab, int j) {
         float r;
-        const f32x2 e = sample(next(), ntab, r);
+        const f32x2 e = sample(j, ntab, r);
         x0 = __builtin_elementwise_fma(f32x2{r, r}, e, x0);
     }
-    __device__ __forceinline__ f32x2 noise(const f32x2* ntab) {
+    __device__ __forceinline__ f32x2 noise(const f32x2* ntab, int j) {
         float r;
-        const f32x2 e = sample(next(), ntab, r);
+        const f32x2 e = sample(j, ntab, r);
         return f32x2{r, r} * e;
     }
     // complex128 without the widened table (the generic kernel, zero-padding tail samples): the
     // same exact product of the float32 radius and entry, fused into the sample
-    __device__ __forceinline__ void add_noise_f64(double& re, double& im, const f32x2* ntab) {
+    __device__ __forceinline__ void add_noise_f64(double& re, double& im, const f32x2* ntab, int j) {
         float r;
-        const f32x2 e = sample(next(), ntab, r);
+        const f32x2 e = sample(j, ntab, r);
         re = __builtin_fma((double)r, (double)e.x, re);
         im = __builtin_fma((double)r, (double)e.y, im);
     }
     // complex128 kernels: the same radius and phase entry, the product taken in double against
     // ntab64 = the float32 table entries widened (exact), fused into the sample: one conversion
-    // and two v_fma_f64 instead of a float product and two conversions.  Bits 3..8 of w address
-    // the 16-byte entries as (w & 0x1F8) * 2.  (16 copies of the table, one per 16-byte bank slot
-    // so that a ds_read_b128 lane group never meets on a bank, measured slower: config b RX
-    // 3.07 -> 3.25 ms, profiles/r03m_ab.txt.)
-    __device__ __forceinline__ void add_noise64(double& re, double& im, const f64x2* ntab64) {
-        const uint32_t w = next();
-        const float r = noise_radius(w);
-        const f64x2 e = *(const f64x2*)((const unsigned char*)ntab64 + 2 * (w & kNoisePhaseMask));
+    // and two v_fma_f64 instead of a float product and two conversions.  (16 copies of the table,
+    // one per 16-byte bank slot so that a ds_read_b128 lane group never meets on a bank, measured
+    // slower: config b RX 3.07 -> 3.25 ms, profiles/r03m_ab.txt.)
+    __device__ __forceinline__ void add_noise64(double& re, double& im, const f64x2* ntab64, int j) {
+        const float r = noise_radius(draw(j));
+        const f64x2 e = *(const f64x2*)((const unsigned char*)ntab64 + phase_off<sizeof(f64x2)>(j));
         const double rd = (double)r;
         re = __builtin_fma(rd, e.x, re);
         im = __builtin_fma(rd, e.y, im);

@@ -393,11 +393,33 @@ __device__ __forceinline__ cpx<R> mmse_coef(cpx<R> hc, R h2, R nv) {
     }
 }
 
+// The lane block of a reference-stream symbol for the throughput kernels' REF instantiations: byte
+// i = the FB bits of element i (subcarrier k = t + i TPS), read MSB first from the caller's byte
+// stream at bit s bps + k FB (the reference's bit order, bits_generation/models.py:26-44 and
+// serial_parallel/models.py:12-33) -- the layout lane_bits reads, so the kernel body is the
+// throughput kernel's.  Global byte reads (uncoalesced: REF runs are parity runs, not timed).
+template <int FB, int TPS>
+__device__ __forceinline__ u4 ref_lane(const TxRxCommon& a, int64_t s, int t) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    const int64_t bit0 = s * a.bps;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t o = bit0 + (int64_t)(t + i * TPS) * FB;
+        const int64_t B = o >> 3;
+        const uint32_t hi = B < a.n_bytes ? (uint32_t)a.bits[B] : 0u;
+        const uint32_t lo = B + 1 < a.n_bytes ? (uint32_t)a.bits[B + 1] : 0u;
+        const uint32_t v = (((hi << 8) | lo) >> (16 - (int)(o & 7) - FB)) & ((1u << FB) - 1u);
+        w[i >> 2] |= v << (8 * (i & 3));
+    }
+    return u4{w[0], w[1], w[2], w[3]};
+}
+
 // Per-element tx constellation indices of one symbol for this lane, from whichever
 // source the launch uses: the lane generator's first 128 bits (philox mode) or the
 // staged words (reference mode).  FB > 0: fixed b = FB, compile-time offsets.  In philox
-// mode the generator g continues into the lane's noise (RX).
-template <int FB, int TPS>
+// mode the generator g continues into the lane's noise (RX).  REF (FB > 1): the throughput
+// kernel's lane block filled from the caller's bits instead (ref_lane).
+template <int FB, int TPS, bool REF = false>
 struct TxBits {
     u4 lane;
     Mwc64x g;
@@ -419,7 +441,9 @@ struct TxBits {
         W = Wslot;
         base_bit = 0;
         lane.x = lane.y = lane.z = lane.w = 0u;
-        if (from_words) {
+        if constexpr (REF && FB > 1) {
+            if (active) lane = ref_lane<FB, TPS>(a, s, t);
+        } else if (from_words) {
             if (active) base_bit = stage_words<TPS>(a, s, Wslot, t);
         } else if (active) {
             seed_lane(a.seed, s, t);
@@ -511,7 +535,8 @@ constexpr bool uses_tt() { return FB > 0 && fast_tt<R, LOGN>(); }
 // Each symbol group walks `chunk` consecutive OFDM symbols so the FIR tail (last L-1
 // stream samples of the previous symbol) is carried in LDS; the first symbol of a chunk
 // regenerates its predecessor's tail (one extra IFFT per chunk, L > 1 only).
-template <typename R, int LOGN, int FB, int LT, bool ZPW = false>
+// REF: the throughput kernel fed the caller's bits (reference streams, ref_lane) -- the same body
+template <typename R, int LOGN, int FB, int LT, bool ZPW = false, bool REF = false>
 __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB, LOGN, LT, ZPW>())) void k_tx(
     TxArgs a) {
     constexpr int BLK = tx_block<R, FB, LOGN, LT, ZPW>();
@@ -617,7 +642,9 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
 #pragma unroll
         for (int q = 0; q < st_sc.K; ++q, k0 += BLK) {
             const ScInfo sc = st_sc.v[q];
-            const int off = __shfl(ax_off, sc.lut < 0 ? 0 : (int)sc.lut);
+            // (a slot past N was never loaded: its lane index is taken as 0, not read)
+            const int lid = k0 < N ? (int)sc.lut : -1;
+            const int off = __shfl(ax_off, lid < 0 ? 0 : lid);
             if (k0 < N) sce[k0] = code(sc, off);
         }
         for (int k = k0; k < N; k += BLK) {
@@ -656,7 +683,7 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
             const int64_t sl = sbeg + c;
             const int64_t sg = cm.sym0 + sl;
             const bool active = grp < ngroups && sl < cm.n_sym && sg >= 0;
-            TxBits<FB, TPS> tb;
+            TxBits<FB, TPS, REF> tb;
             tb.load(cm, sg, t, W, active && !(flags & 1));
             if (FB == 0) sym_sync<TPS>();  // staged words visible
             // map (QAMConstellationMapper.encode, constellation/models.py:240-246); the
@@ -1120,7 +1147,8 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
 // EQ: OFDM_EQ_* fixed at compile time (throughput kernel) or -1 = from the plan.
 // MV: SC-OFDM and zero padding compiled in (run-time flags); complex128 compiles them out of the
 // cyclic-prefix OFDM kernels (rx_eq)
-template <typename R, int LOGN, int EQ, int FB, bool MV>
+// REF: the throughput kernel fed the caller's bits and normals (reference streams) -- the same body
+template <typename R, int LOGN, int EQ, int FB, bool MV, bool REF = false>
 __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB, LOGN, EQ, MV>())) void k_rx(
     RxArgs a) {
     constexpr int BLK = rx_block<R, FB, LOGN, EQ, MV>();
@@ -1141,8 +1169,8 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
     const int ystride = (FB == 1 || !MV) ? N : cm.ystride;
     // odd bits per subcarrier (FB = 3, 5): the reference's 8- / 32-PSK only
     constexpr bool FB_PSK_ONLY = FB > 1 && (FB & 1);
-    // noise phase table: static LDS at a link-time constant address, so a lane word's bits 3..8
-    // (its byte offset) address an entry with no add
+    // noise phase table: static LDS at a link-time constant address, so a sample's entry offset
+    // (from its phase word) addresses it with no add
     __shared__ f32x2 ntab[kNoisePhases];
     // complex128 throughput kernels: the table widened to double (Mwc64x::add_noise64)
     __shared__ f64x2 ntab64_s[F64_FAST ? kNoisePhases : 1];
@@ -1281,7 +1309,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
         slicer.load(axis[0]);
     }
 
-    const bool array_noise = FB == 0 && a.nr != nullptr && noise;
+    const bool array_noise = (FB == 0 || REF) && a.nr != nullptr && noise;
     const int64_t niter = (cm.n_sym + G::SPB - 1) / G::SPB;
     unsigned long long be = 0, se = 0;
 
@@ -1323,7 +1351,7 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
         const int64_t sl = it * G::SPB + ls;
         const int64_t sg = cm.sym0 + sl;
         const bool active = sl < cm.n_sym;
-        TxBits<FB, TPS> tb;
+        TxBits<FB, TPS, REF> tb;
         // kept channel samples + AWGN; the 1/sqrt(N) of fft(norm="ortho") folded in
         const C* ys = (const C*)a.y + sl * ystride;
         C x[E];
@@ -1338,21 +1366,23 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                 x[i].im += sigma * (R)ni[t + i * TPS];
             }
         } else if (active && noise) {
-            // one lane word per element (stream outputs m2 .. m(E+1))
+            // noise sample j = i of the lane: a radius word per element, a phase word per four
+            // (stream version 3, ofdm_device.hpp "throughput-mode streams")
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 if constexpr (sizeof(R) == 4) {
-                    tb.g.add_noise(x[i].v, ntab);
+                    tb.g.add_noise(x[i].v, ntab, i);
                 } else if constexpr (F64_FAST) {
-                    tb.g.add_noise64(x[i].re, x[i].im, ntab64);
+                    tb.g.add_noise64(x[i].re, x[i].im, ntab64, i);
                 } else {
-                    tb.g.add_noise_f64(x[i].re, x[i].im, ntab);
+                    tb.g.add_noise_f64(x[i].re, x[i].im, ntab, i);
                 }
             }
         }
         if (zp && active) {
             // zero guard: received sample N + k (k < cp) is added onto sample k, noise included
-            // (philox mode: one more lane word per tail sample, after the elements' noise)
+            // (philox mode: the lane's noise samples continue, tail sample i is sample E + i -- the
+            // tail samples a lane owns are its first ones, k < cp)
 #pragma unroll
             for (int i = 0; i < E; ++i) {
                 const int k = t + i * TPS;
@@ -1363,9 +1393,9 @@ __global__ __launch_bounds__((rx_block<R, FB, LOGN, EQ, MV>()), (rx_waves<R, FB,
                         v.im += sigma * (R)a.ni[sg * (N + cp) + N + k];
                     } else if (noise) {
                         if constexpr (sizeof(R) == 8) {
-                            tb.g.add_noise_f64(v.re, v.im, ntab);
+                            tb.g.add_noise_f64(v.re, v.im, ntab, E + i);
                         } else {
-                            const f32x2 n = tb.g.noise(ntab);
+                            const f32x2 n = tb.g.noise(ntab, E + i);
                             v = v + mk<R>(n.x, n.y);
                         }
                     }

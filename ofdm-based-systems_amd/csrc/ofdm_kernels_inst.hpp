@@ -37,6 +37,14 @@ static hipError_t set_smem(F fn, size_t bytes) {
     return e;
 }
 
+// a log2 N outside the build's cases: a plan never asks for one in a product build (N is checked at
+// plan creation); an OFDM_AB_ONLY build lacks N < 1024 (kNotInBuild)
+#ifdef OFDM_AB_ONLY
+constexpr hipError_t kOutOfRange = kNotInBuild;
+#else
+constexpr hipError_t kOutOfRange = hipErrorInvalidValue;
+#endif
+
 constexpr int kFastMinLogN = 6;  // throughput specialisations for N >= 64
 // LDS per CU on gfx950: a throughput-kernel instantiation whose LDS would exceed it (a shape the plan
 // allows but the specialised layout cannot hold) runs the generic kernel instead of failing at
@@ -69,7 +77,7 @@ hipError_t launch_rows(int logn, int mode, const RowsArgs& a, hipStream_t s) {
     switch (logn) {
         OFDM_LOGN_CASES(OFDM_ROWS_CASE)
         default:
-            return hipErrorInvalidValue;
+            return kOutOfRange;
     }
 #undef OFDM_ROWS_CASE
 }
@@ -179,7 +187,7 @@ static inline int fused_grid(int64_t want, int resident) {
     return clamp_grid(want);
 }
 
-template <typename R, int LOGN, int FB, int LT, bool ZPW = false>
+template <typename R, int LOGN, int FB, int LT, bool ZPW = false, bool REF = false>
 static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     constexpr int BLK = tx_block<R, FB, LOGN, LT, ZPW>();
     TxArgs a = a0;
@@ -202,7 +210,7 @@ static hipError_t tx_launch(const TxArgs& a0, int* grid, hipStream_t s) {
     if constexpr (FB > 0) {
         if (sm + tx_static_lds<R, FB, LT>() > kLdsPerCu) return tx_launch<R, LOGN, 0, -1>(a0, grid, s);
     }
-    auto fn = k_tx<R, LOGN, FB, LT, ZPW>;
+    auto fn = k_tx<R, LOGN, FB, LT, ZPW, REF>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     const int resident = resident_blocks(fn, BLK, sm);
@@ -235,12 +243,42 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
     return tx_launch<R, LOGN, FB, -1>(a, grid, s);
 }
 
+// Reference streams (the caller's bits; RX: and normals) on the bench configs' shapes go through the
+// throughput kernels' REF instantiations -- the timed kernels' bodies with the bit and noise source
+// swapped (ref_lane, array normals) -- so the reference's own streams pin the benched FFT / FIR /
+// slicer / count code (tests/test_gpu_ref_streams.py): complex128, OFDM with a cyclic prefix, fixed
+// 64-QAM at N = 1024 (configs b, c) and 256-QAM at N = 4096 (config e), flat or <= 8-tap channels
+// within the window FIR's reach.  Everything else with caller bits takes the generic kernel.
+template <typename R, int LOGN>
+constexpr int ref_fb() { return sizeof(R) == 8 ? (LOGN == 10 ? 6 : LOGN == 12 ? 8 : 0) : 0; }
+
+template <typename R, int LOGN>
+static bool ref_shape(const TxRxCommon& c) {
+    return ref_fb<R, LOGN>() > 0 && c.bits != nullptr && !c.adaptive && !c.nn && c.psk_m == 0 && !c.scm && !c.zpad &&
+           c.b == ref_fb<R, LOGN>();
+}
+
+template <typename R, int LOGN>
+static hipError_t tx_ref(const TxArgs& a, int* grid, hipStream_t s) {
+    constexpr int FB = ref_fb<R, LOGN>();
+    if constexpr (FB > 0) {
+        constexpr int TPS = Geo<LOGN>::TPS;
+        if (a.L == 1) return tx_launch<R, LOGN, FB, 0, false, true>(a, grid, s);
+        if (a.c.cp <= TPS) {
+            if (a.L <= 4) return tx_launch<R, LOGN, FB, 4, false, true>(a, grid, s);
+            if (a.L <= 8) return tx_launch<R, LOGN, FB, 8, false, true>(a, grid, s);
+        }
+    }
+    return tx_launch<R, LOGN, 0, -1>(a, grid, s);
+}
+
 // Throughput configuration (complex64, fixed square QAM or the reference's 4/8/16/32-PSK (psk_m > 0),
 // Philox bits; N >= 64; OFDM or SC-OFDM, cyclic prefix or zero padding) -> the kernel specialised on the bits per
 // subcarrier; adaptive bit loading over the reference's square-QAM LUTs (OFDM, cyclic
 // prefix) -> the adaptive throughput kernel (FB = 1); anything else -> the generic kernel.
 template <typename R, int LOGN>
 static hipError_t tx_one(const TxArgs& a, int* grid, hipStream_t s) {
+    if (ref_shape<R, LOGN>(a.c)) return tx_ref<R, LOGN>(a, grid, s);
     if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
         // complex128 throughput kernels: device bits; square QAM with adaptive loading (OFDM, cyclic
         // prefix); fixed square QAM or the reference's 4..32-PSK, OFDM or SC-OFDM, cyclic prefix or
@@ -284,12 +322,12 @@ hipError_t launch_tx(int logn, const TxArgs& a, int* grid, hipStream_t s) {
     switch (logn) {
         OFDM_LOGN_CASES(OFDM_TX_CASE)
         default:
-            return hipErrorInvalidValue;
+            return kOutOfRange;
     }
 #undef OFDM_TX_CASE
 }
 
-template <typename R, int LOGN, int EQ, int FB, bool MV>
+template <typename R, int LOGN, int EQ, int FB, bool MV, bool REF = false>
 static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     constexpr int BLK = rx_block<R, FB, LOGN, EQ, MV>();
     const size_t sm = smem_rx<R>(LOGN, BLK, a.c.words_per_sym,
@@ -300,7 +338,7 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
     if constexpr (FB > 0) {
         if (sm + rx_static_lds<R, FB>() > kLdsPerCu) return rx_launch<R, LOGN, -1, 0, true>(a, grid, s);
     }
-    auto fn = k_rx<R, LOGN, EQ, FB, MV>;
+    auto fn = k_rx<R, LOGN, EQ, FB, MV, REF>;
     hipError_t e = set_smem(fn, sm);
     if (e != hipSuccess) return e;
     const int64_t want = (a.c.n_sym + Geo<LOGN, BLK>::SPB - 1) / Geo<LOGN, BLK>::SPB;
@@ -315,11 +353,11 @@ static hipError_t rx_launch(const RxArgs& a, int* grid, hipStream_t s) {
 // MV: the run-time modem variants (SC-OFDM, zero padding) compiled in.  complex128 builds them as
 // separate kernels: compiled into the cyclic-prefix OFDM kernels of the bench, their second
 // transform and guard overlap-add spilled the config (b) receiver (~70 dwords at 128 VGPRs)
-template <typename R, int LOGN, int FB, bool MV = true>
+template <typename R, int LOGN, int FB, bool MV = true, bool REF = false>
 static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
-    if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, FB, MV>(a, grid, s);
-    if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, FB, MV>(a, grid, s);
-    return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB, MV>(a, grid, s);
+    if (a.c.eq == OFDM_EQ_NONE) return rx_launch<R, LOGN, OFDM_EQ_NONE, FB, MV, REF>(a, grid, s);
+    if (a.c.eq == OFDM_EQ_ZF) return rx_launch<R, LOGN, OFDM_EQ_ZF, FB, MV, REF>(a, grid, s);
+    return rx_launch<R, LOGN, OFDM_EQ_MMSE, FB, MV, REF>(a, grid, s);
 }
 
 // Throughput configuration (complex64, fixed square QAM or the reference's 4/8/16/32-PSK (psk_m > 0),
@@ -327,6 +365,12 @@ static hipError_t rx_eq(const RxArgs& a, int* grid, hipStream_t s) {
 // equaliser; anything else -> the generic kernel.
 template <typename R, int LOGN>
 static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
+    if constexpr (ref_fb<R, LOGN>() > 0) {
+        // reference streams on a bench shape (see ref_shape): the REF receiver needs the caller's
+        // normals and no received-symbol tap
+        if (ref_shape<R, LOGN>(a.c) && a.nr != nullptr && a.z_out == nullptr)
+            return rx_eq<R, LOGN, ref_fb<R, LOGN>(), false, true>(a, grid, s);
+    }
     if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
             !a.c.scm && !a.c.zpad && !a.c.nn)
@@ -371,7 +415,7 @@ hipError_t launch_rx(int logn, const RxArgs& a, int* grid, hipStream_t s) {
     switch (logn) {
         OFDM_LOGN_CASES(OFDM_RX_CASE)
         default:
-            return hipErrorInvalidValue;
+            return kOutOfRange;
     }
 #undef OFDM_RX_CASE
 }

@@ -214,6 +214,16 @@ inline size_t smem_rx(int logn, int blk, int wps, int tts, size_t extra /* adapt
            rnd16((size_t)tts * c) + rnd16(extra);
 }
 
+// A launcher's answer for a shape its build does not instantiate (OFDM_AB_ONLY experiment builds:
+// N = 1024..4096 only); the ABI reports it as OFDM_E_INVALID "kernel not in this build".  Product
+// builds instantiate every shape a plan accepts and never return it.
+#ifdef OFDM_AB_ONLY
+constexpr bool kAbOnly = true;
+#else
+constexpr bool kAbOnly = false;
+#endif
+constexpr hipError_t kNotInBuild = hipErrorNotSupported;  // (only ever meant so when kAbOnly)
+
 // ---- launchers (instantiated for float and double in ofdm_kernels_f{32,64}.hip)
 template <typename R>
 hipError_t launch_rows(int logn, int mode, const RowsArgs& a, hipStream_t s);

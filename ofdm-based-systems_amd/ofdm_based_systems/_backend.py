@@ -24,7 +24,9 @@ import torch
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
                          "libofdm_hip%s.so" % ("_" + os.environ["OFDM_LIB_VARIANT"]
                                                if os.environ.get("OFDM_LIB_VARIANT") else ""))
-ABI_VERSION = 4
+# ABI 5: throughput-mode stream version 3 (the noise radius takes the whole lane word, the phase
+# its own word per four samples; csrc/ofdm_device.hpp "throughput-mode streams")
+ABI_VERSION = 5
 
 OFDM_F32, OFDM_F64 = 0, 1
 # ofdm_stats (include/ofdm_hip.h): power_sum, x_power_sum, x_peak (double), power_fx[2] (int64)
@@ -145,7 +147,12 @@ def load_library() -> ctypes.CDLL:
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        if handle.ofdm_abi_version() != ABI_VERSION:
+        # (a variant build of an earlier round -- same entry points, earlier stream version -- is
+        # accepted for A/B studies when OFDM_LIB_VARIANT_ABI names its version)
+        want = ABI_VERSION
+        if os.environ.get("OFDM_LIB_VARIANT") and os.environ.get("OFDM_LIB_VARIANT_ABI"):
+            want = int(os.environ["OFDM_LIB_VARIANT_ABI"])
+        if handle.ofdm_abi_version() != want:
             raise BackendUnavailable("libofdm_hip ABI version mismatch")
         _lib = handle
         return handle

@@ -13,7 +13,7 @@ fused throughput kernels are checked against the oracle on identical bits and no
 Like ``ofdm_oracle`` it is the CHECKER: only ``tests/``, ``__graft_entry__.smoke()`` and
 ``bench.py``'s ``cpu_baseline`` leg may import it.
 
-Definition (stream version 2; one OFDM symbol s of N subcarriers, E = min(16, N) elements
+Definition (stream version 3; one OFDM symbol s of N subcarriers, E = min(16, N) elements
 per lane, TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS for i < E):
 
 * lane block: words P0..P3 of one Philox4x32-10 block, key = (seed mod 2^32, seed >> 32),
@@ -24,14 +24,22 @@ per lane, TPS = N / E lanes; lane t owns subcarrier / time sample k = t + i*TPS 
 * payload: the 128 bits (P2, P3, m0, m1); element i takes the low b bits of byte i (byte i =
   bits 8*(i & 3).. of word i >> 2); with adaptive bit loading b = b_k of its subcarrier
   (b_k = 0: the subcarrier is unused and carries 0+0j);
-* noise: element i gets the complex normal of word w = m(2 + i), added to the kept time
-  sample k: radius sqrt(32 - log2(float32(w | 0x1F8))) (i.e. sqrt(-2 ln u) / sqrt(2 ln 2) with
-  u = (w | 0x1F8) 2^-32), times table entry j = (w >> 3) & 63, where entry j is
-  float32(sigma sqrt(2 ln 2)) * float32(cos, sin)(2 pi (j + 1/2) / 64) in float32.  (float32
-  arithmetic on the GPU, with the hardware log2 / sqrt; here the radius argument follows the
-  same float32 rounding of the word and the rest is evaluated in float64.)
-* zero padding: after the elements' noise a lane draws one more word per received tail
-  sample N + k it owns (k = t + i*TPS < cp, in order of i).
+* noise: the generator continues into the lane's noise samples n = 0, 1, ... (element i is
+  sample i, added to the kept time sample k): before samples n = 0, 4, 8, ... the lane draws a
+  phase word q, then every sample draws its radius word w (outputs m2 = q, m3..m6 = w for samples
+  0..3, m7 = the next q, ...).  Sample n is radius sqrt(32 - log2(float32(w | 1))) (i.e.
+  sqrt(-2 ln u) / sqrt(2 ln 2) with u = (w | 1) 2^-32) times table entry j = (q >> 8 (n & 3)) & 63,
+  where entry j is float32(sigma sqrt(2 ln 2)) * float32(cos, sin)(2 pi (j + 1/2) / 64) in float32.
+  (float32 arithmetic on the GPU, with the hardware log2 / sqrt; here the radius argument follows
+  the same float32 rounding of the word and the rest is evaluated in float64.)  u runs over the
+  odd multiples of 2^-32 (words 2k and 2k + 1 share u = (2k + 1) 2^-32): the radius is the
+  Rayleigh quantile at the midpoints of 2^31 equiprobable cells, so P(radius > x) is exact at every
+  cell boundary -- the deepest at 6.555 sigma (P = 2^-31; its cell's mass sits at 6.660 sigma) --
+  and within one cell (2^-31) between them.
+  (Stream version 2 took the phase from bits 3..8 of the radius word, which truncated the radius
+  at 5.65 sigma.)
+* zero padding: after the elements' noise the lane's samples continue with the received tail
+  samples N + k it owns (k = t + i*TPS < cp, in order of i): tail sample i is noise sample E + i.
 """
 
 from __future__ import annotations
@@ -68,7 +76,7 @@ def philox4x32_10(c0, c1, c2, c3, k0: int, k1: int):
 
 MWC_A = np.uint64(4294883355)
 NOISE_PHASES = 64
-NOISE_MASK = np.uint32(0x1F8)
+RADIUS_OR = np.uint32(1)  # u = (w | 1) 2^-32: word 0 joins word 1, u > 0
 SQRT_2LN2 = 1.1774100225154747
 
 # Deviations of a point beyond this many standard deviations of z_stat_bound's model are not
@@ -99,9 +107,22 @@ class LaneStream:
     def __init__(self, p0, p1, p2, p3):
         self.gen = Mwc64x(p0, p1)
         self.payload = np.stack([p2, p3, self.gen.next(), self.gen.next()], axis=1).astype(np.uint32)
+        self.n = 0      # next noise sample of every lane
+        self.q = None   # its phase word
 
     def next(self) -> np.ndarray:
         return self.gen.next()
+
+    def noise_draw(self):
+        """(radius word, phase index) of every lane's next noise sample n: the phase word q is
+        drawn before samples n = 0 mod 4, the radius word w by every sample; phase = byte n & 3 of q,
+        low six bits."""
+        if self.n % 4 == 0:
+            self.q = self.gen.next()
+        w = self.gen.next()
+        ph = (self.q >> np.uint32(8 * (self.n % 4))) & np.uint32(NOISE_PHASES - 1)
+        self.n += 1
+        return w, ph
 
 
 def geometry(N: int):
@@ -129,10 +150,10 @@ def noise_table(sigma: float) -> np.ndarray:
     return re.astype(np.float64) + 1j * im.astype(np.float64)
 
 
-def noise_from_words(w: np.ndarray, sigma: float, with_bound: bool = False, radius_fn=None,
+def noise_from_words(w: np.ndarray, ph: np.ndarray, sigma: float, with_bound: bool = False, radius_fn=None,
                      product_rel: float = 2.0 ** -24):
-    """Complex normal of each 32-bit lane word (radius from the word with bits 3..8 set,
-    phase = bits 3..8 through the table).
+    """Complex normal of each noise sample: radius from its 32-bit radius word w (u = (w | 1) 2^-32),
+    phase = table entry ph (0..63, from the lane's phase word).
 
     radius_fn: None -> the radius sqrt(32 - log2(f)) in float64 from the word's float32 value f;
     otherwise a function mapping the words to the float32 radii the GPU's hardware log2 / sqrt
@@ -149,12 +170,12 @@ def noise_from_words(w: np.ndarray, sigma: float, with_bound: bool = False, radi
       receivers round it once (product_rel 2^-24).  The table is the GPU's bit for bit when sigma is (float32 entries
       of the same double sigma, tests/test_oracle_philox.py::test_noise_table_entries_are_robust)."""
     w = np.asarray(w, np.uint32)
-    e = noise_table(sigma)[(w >> np.uint32(3)) & np.uint32(NOISE_PHASES - 1)]
+    e = noise_table(sigma)[np.asarray(ph, np.int64)]
     if radius_fn is not None:
         r = np.asarray(radius_fn(w), np.float32).astype(np.float64)
         n = r * e
         return (n, product_rel * np.abs(n)) if with_bound else n
-    f = (w | NOISE_MASK).astype(np.float32)  # round to nearest even, as v_cvt_f32_u32
+    f = (w | RADIUS_OR).astype(np.float32)  # round to nearest even, as v_cvt_f32_u32
     A = 32.0 - np.log2(f.astype(np.float64))
     r = np.sqrt(A)
     n = r * e
@@ -184,10 +205,10 @@ def tx_indices(gen: LaneStream, S: int, N: int, b) -> np.ndarray:
 
 def lane_noise(gen: LaneStream, S: int, N: int, sigma: float, with_bound: bool = False, radius_fn=None,
                product_rel: float = 2.0 ** -24):
-    """Complex noise (S, N) at the kept time samples, from outputs m2 .. m(E+1) of every lane
+    """Complex noise (S, N) at the kept time samples, noise samples 0 .. E-1 of every lane
     (with_bound: and the (S, N) bound of noise_from_words)."""
     E, _ = geometry(N)
-    parts = [noise_from_words(gen.next(), sigma, with_bound, radius_fn, product_rel) for _ in range(E)]
+    parts = [noise_from_words(*gen.noise_draw(), sigma, with_bound, radius_fn, product_rel) for _ in range(E)]
     if not with_bound:
         return _lane_to_row(np.stack(parts, axis=1), S, N)
     return (_lane_to_row(np.stack([p[0] for p in parts], axis=1), S, N),
@@ -218,9 +239,9 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
     """Global OFDM symbols [0, S) of a throughput-mode run, through the oracle arithmetic.
 
     modulator "OFDM" | "SC" (modulation/models.py:58-91), prefix "CP" | "ZP"
-    (prefix/models.py:29-101), scheme "QAM" | "PSK".  With zero padding every lane draws,
-    after its elements' noise, one more noise word per received tail sample
-    N + k (k = t + i*TPS < cp, in order of i).
+    (prefix/models.py:29-101), scheme "QAM" | "PSK".  With zero padding every lane's noise
+    samples continue, after its elements', with the received tail samples N + k it owns
+    (k = t + i*TPS < cp, in order of i).
 
     orders: per-subcarrier QAM orders (CAPACITY_BASED bit loading, 0 = unused; M is then
     ignored).  As in the reference's decode (constellation/adaptive.py:259-263) a trailing
@@ -293,8 +314,8 @@ def run_philox(seed: int, S: int, N: int, M: int, h_raw: np.ndarray, cp: int, eq
             t = np.tile(np.arange(tps), S)
             for i in range(E):
                 k = t + i * tps
-                w = gen.next()
-                n, nb = noise_from_words(w, sigma, with_bound=True, radius_fn=radius_fn, product_rel=prel)
+                w, ph = gen.noise_draw()  # noise sample E + i
+                n, nb = noise_from_words(w, ph, sigma, with_bound=True, radius_fn=radius_fn, product_rel=prel)
                 use = k < cp
                 srow = np.repeat(np.arange(S), tps)[use]
                 tail[srow, k[use]] += n[use]

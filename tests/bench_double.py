@@ -39,7 +39,11 @@ class LazyStreamEngine(OracleEngine):
 
 
 def make_engine(cfg, precision):
+    """The double of bench.make_engine.  CAPACITY_BASED configs (M = 0: config d) run a fixed 16-QAM
+    stand-in -- the double checks the bench's rank launch, sweep groups and reporting, not the
+    adaptive loading, which the GPU tests hold to the oracle and the reference."""
     N, M, ch, ratio, eq, snr, _ = cfg
+    M = M or 16
     h = np.load(os.path.join(ROOT, "config", "channel_models", ch + ".npy"))
     cp = int(ratio * (len(h) - 1))
     return LazyStreamEngine(N, M, h, cp, eq)

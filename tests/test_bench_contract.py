@@ -132,3 +132,46 @@ def test_bench_sweep_config_e_two_ranks():
     assert sw["points"] == 15 and sw["snr_db"] == bench.SWEEP_SNRS_E * 3
     assert [p["qam_order"] for p in sw["per_point"]] == [16] * 5 + [64] * 5 + [256] * 5
     assert d["ber_1e-4_crossing_db"] is None
+
+
+def _bench(args, timeout=900):
+    """Run bench.py with the CPU engine double (gloo ranks); returns the JSON line."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
+                                         os.path.join(ROOT, "ofdm-based-systems_amd"), env.get("PYTHONPATH", "")])
+    env.pop("WORLD_SIZE", None)
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--backend", "gloo",
+                        "--engine-factory", "bench_double:make_engine", "--no-ber-check", "--ramp-seconds", "0"] + args,
+                       env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout
+    return json.loads(line[0])
+
+
+@pytest.mark.parametrize("config,sweep", [("b", False), ("c", True), ("d", True), ("e", True)])
+def test_bench_eight_ranks_count_what_one_rank_counts(config, sweep):
+    """The N = 8 line the driver's scaling run prints, rehearsed with 8 gloo ranks on the CPU engine
+    double: n_gpus / devices / symbols per step follow the rank count, the CPU baseline is on the
+    line, and with the same global symbols per point (8 ranks x 1 symbol against 1 rank x 8 -- the
+    streams are per symbol, the power exchange exact) every point's BER equals the one-rank run's."""
+    extra = ["--sweep"] if sweep else ["--no-variant"]
+    common = ["--config", config, "--steps", "1", "--warmup", "0", "--cpu-sample", "1"] + extra
+    d8 = _bench(["--gpus", "8", "--symbols", "1"] + common)
+    d1 = _bench(["--gpus", "1", "--symbols", "8"] + common)
+    npts = d8["sweep"]["points"] if sweep else 1
+    assert d8["n_gpus"] == 8 and d8["devices"] == ["cpu"] * 8 and d1["n_gpus"] == 1
+    assert d8["config"]["symbols_per_step"] == d1["config"]["symbols_per_step"] == 8 * npts
+    assert d8["scaling"] == "weak" and d8["value"] > 0
+    cb = d8["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port"
+    if sweep:
+        assert d8["sweep"]["snr_db"] == d1["sweep"]["snr_db"]
+        assert d8["sweep"]["ber"] == d1["sweep"]["ber"]
+        assert [p["bits"] for p in d8["sweep"]["per_point"]] == [p["bits"] for p in d1["sweep"]["per_point"]]
+    else:
+        assert d8["ber"] == d1["ber"]

@@ -1,4 +1,4 @@
-"""The --sweep groups of configs d and e on the GPU (bench.measure_sweep in-process, small sizes):
+"""The --sweep groups of configs c, d and e on the GPU (bench.measure_sweep in-process, small sizes):
 every point of every group is one complete run of its own engine, so its counts equal a plain
 LinkEngine.run of that engine with the same seed (the sweep only schedules: pipelining over two
 lanes, all groups enqueued before any count is read)."""
@@ -13,7 +13,7 @@ import bench
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["d", "e"])
+@pytest.mark.parametrize("name", ["c", "d", "e"])
 def test_sweep_groups_count_what_single_runs_count(gpu, name):
     os.environ.pop("WORLD_SIZE", None)
     rt = bench.Runtime("nccl", cpu=False)
@@ -36,5 +36,10 @@ def test_sweep_groups_count_what_single_runs_count(gpu, name):
             i += 1
     if name == "e":
         assert [p["qam_order"] for p in sw["per_point"]] == [16] * 5 + [64] * 5 + [256] * 5
-    else:
+        assert sw["bits_per_point"] == [e.valid_bits(per_gpu) * 2 for e in engines]
+    elif name == "d":
         assert [p["qam_order"] for p in sw["per_point"]] == ["adaptive"] * 3
+    else:  # config (c): BASELINE configs[2]'s 40-point 0..30 dB sweep on one 64-QAM engine
+        assert [p["snr_db"] for p in sw["per_point"]] == bench.SWEEP_GRID and len(groups) == 1
+        assert [p["qam_order"] for p in sw["per_point"]] == [64] * 40
+        assert sw["bits_per_point"] == engines[0].valid_bits(per_gpu) * 2

@@ -78,3 +78,27 @@ def test_bench_two_ranks_on_one_gpu(gpu):
     assert d["n_gpus"] == 2 and d["devices"] == [0, 0], d
     assert d["config"]["symbols_per_step"] == 200_000 and d["scaling"] == "weak" and d["value"] > 0
     assert d["dtype"].startswith("c128") and 1e-5 < d["ber"] < 1e-3
+
+
+@pytest.mark.parametrize("config", ["c", "d", "e"])
+def test_bench_sweep_two_ranks_on_one_gpu(gpu, config):
+    """bench.py --gpus 2 --sweep on device 0 (gloo; the rehearsal of the driver's multi-GPU sweep
+    line): every point's BER equals the one-rank sweep's over the same global symbols (2 ranks x S
+    against 1 rank x 2S), and the line carries n_gpus / devices of the two ranks."""
+    per = {"c": 2000, "d": 1000, "e": 500}[config]
+    common = ["--sweep", "--config", config, "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+              "--no-ber-check"]
+    r = _launch([os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--symbols", str(per)] + common,
+                timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d2 = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    env = _env()
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--symbols", str(2 * per)] + common,
+                        env=env, capture_output=True, text=True, timeout=600)
+    assert r1.returncode == 0, r1.stderr[-4000:]
+    d1 = json.loads([x for x in r1.stdout.splitlines() if x.startswith("{")][0])
+    assert d2["n_gpus"] == 2 and d2["devices"] == [0, 0] and d1["n_gpus"] == 1
+    assert d2["config"]["symbols_per_step"] == d1["config"]["symbols_per_step"]
+    assert d2["sweep"]["snr_db"] == d1["sweep"]["snr_db"]
+    assert d2["sweep"]["ber"] == d1["sweep"]["ber"], (d2["sweep"]["ber"], d1["sweep"]["ber"])
+    assert d2["roofline"] is not None and d2["value"] > 0

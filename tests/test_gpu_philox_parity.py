@@ -252,12 +252,16 @@ def test_gpu_noise_radius_within_its_bound(gpu):
     (noise_from_words) on 2^22 words spread over the whole 32-bit range, and is exact at 0."""
     rng = np.random.default_rng(5)
     w = np.concatenate([rng.integers(0, 2 ** 32, size=1 << 22, dtype=np.uint64).astype(np.uint32),
-                        np.array([0, 1, 0x1F8, 0xFFFFFE07, 0xFFFFFFFF], np.uint32)])
-    n64, b64 = P.noise_from_words(w, 1.0, with_bound=True)
-    n32 = P.noise_from_words(w, 1.0, radius_fn=gpu_radius)
+                        np.arange(0, 4096, dtype=np.uint32),
+                        np.array([0x1F8, 0xFFFFFE07, 0xFFFFFF7F, 0xFFFFFF80, 0xFFFFFFFF], np.uint32)])
+    ph = rng.integers(0, P.NOISE_PHASES, size=w.size)
+    n64, b64 = P.noise_from_words(w, ph, 1.0, with_bound=True)
+    n32 = P.noise_from_words(w, ph, 1.0, radius_fn=gpu_radius)
     assert np.all(np.abs(n32 - n64) <= b64)
     r = gpu_radius(w)
-    assert np.all(np.isfinite(r)) and r.min() >= 0.0 and r.max() < 5.66 / P.SQRT_2LN2
+    # stream version 3: the whole word -- 6.660 sigma at words 0 / 1, 6.493 sigma at words 2 / 3
+    assert np.all(np.isfinite(r)) and r.min() >= 0.0 and r.max() < 6.661 / P.SQRT_2LN2
+    assert r[(1 << 22) + 0] == r[(1 << 22) + 1] and abs(r[(1 << 22) + 2] * P.SQRT_2LN2 - 6.4934) < 1e-3
 
 
 def test_sharded_halves_add_up_to_the_whole(gpu):

@@ -84,21 +84,82 @@ def test_phase_table_projection_tails(phi):
 
 
 def test_radius_words():
-    """radius^2 sigma^2 2 ln2 (32 - log2(w | 0x1F8)) = -2 sigma^2 ln u, u = (w | 0x1F8) 2^-32;
-    truncated at u = 504 2^-32 (5.65 sigma); zero for the words whose float32 rounds to 2^32
-    (w >= 0xFFFFFF80: 2^-25 of the words).  The component tail beyond ~4.5 sigma is depleted
-    by the truncation, so throughput-mode BER is valid down to ~1e-7."""
-    w = np.array([0, 0x1F8, 0xFFFFFFFF, 1 << 20], np.uint32)
-    n = P.noise_from_words(w, 1.0)
-    u = (w | 0x1F8).astype(np.float64) / 2.0 ** 32
-    u[2] = 1.0  # float32(0xFFFFFFFF) rounds to 2^32
+    """radius^2 sigma^2 2 ln2 (32 - log2(w | 1)) = -2 sigma^2 ln u, u = (w | 1) 2^-32 (stream
+    version 3: the radius takes the whole word; u runs over the odd multiples of 2^-32, the
+    midpoints of 2^31 equiprobable cells); the largest radius is 6.660 sigma (words 0 and 1), the
+    next 6.493 sigma (words 2 and 3); zero for the words whose float32 rounds to 2^32
+    (w >= 0xFFFFFF80: 2^-25 of the words)."""
+    w = np.array([0, 1, 2, 0x1F8, 0xFFFFFFFF, 1 << 20], np.uint32)
+    n = P.noise_from_words(w, np.zeros(len(w), np.int64), 1.0)
+    u = (w | 1).astype(np.float64) / 2.0 ** 32
+    u[4] = 1.0  # float32(0xFFFFFFFF) rounds to 2^32
     assert np.allclose(np.abs(n), np.sqrt(-2 * np.log(u)), rtol=1e-6)
-    assert abs(np.abs(n[0]) - 5.6498) < 1e-3
-    assert np.abs(n[2]) == 0.0
+    assert abs(np.abs(n[0]) - 6.6604) < 1e-3 and np.abs(n[1]) == np.abs(n[0])
+    assert abs(np.abs(n[2]) - 6.4934) < 1e-3
+    assert np.abs(n[4]) == 0.0
+
+
+def _radius_sf_on_words(x: float) -> float:
+    """P(radius > x sigma) over the 2^32 radius words of stream version 3, counted exactly: the
+    radius falls with float32(w | 1), so it exceeds x for the words below the first w whose float32
+    value reaches 2^32 exp(-x^2 / 2) (binary search on the monotone map)."""
+    t = 2.0 ** 32 * np.exp(-x * x / 2)
+    lo, hi = 0, 2 ** 32  # invariant: f(lo - 1) < t <= f(hi), f(w) = float32(w | 1)
+    f = lambda v: float(np.float32(np.uint32(v) | np.uint32(1)))
+    if f(0) >= t:
+        return 0.0
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if f(mid) < t:
+            lo = mid
+        else:
+            hi = mid
+    # words 0..lo have f < t (lo is the last such word); the radius at f exactly t equals x
+    return (lo + 1) / 2.0 ** 32
+
+
+@pytest.mark.parametrize("x", [1.0, 3.0, 4.5, 5.0, 5.65, 6.0, 6.3, 6.5, 6.55])
+def test_radius_tail_is_rayleigh_to_6_5_sigma(x):
+    """Stream version 3's radius is the Rayleigh quantile at the midpoints of 2^31 equiprobable cells
+    of u: P(radius > x) = exp(-x^2 / 2) to within one cell (2^-31) plus the float32 rounding of u
+    (relative 2^-24) for every x, exact at each cell boundary, the deepest at 6.555 sigma (P = 2^-31);
+    version 2 had nothing left beyond 5.65 sigma."""
+    want = np.exp(-x * x / 2)
+    got = _radius_sf_on_words(x)
+    assert abs(got - want) <= 2.0 ** -31 + 2.0 ** -23 * want, (x, got, want)
+
+
+def test_component_tail_to_6_2_sigma():
+    """The component tail the deep-BER checks rest on: P(Re n > d sigma) = (1/64) sum_j P(radius >
+    d / cos theta_j) over the phase points with cos > 0, from the exact word counts, against the
+    Gaussian Q(d): within 2^-33 absolute at every depth to 6.2 sigma (measured: < 0.15 x 2^-32), so
+    within 1e-3 relative to d = 5.5 (BER ~1e-8 at 64-QAM) -- where version 2's truncated radius had
+    lost the whole tail beyond 5.65 sigma."""
+    th = 2 * np.pi * (np.arange(P.NOISE_PHASES) + 0.5) / P.NOISE_PHASES
+    c = np.cos(th)
+    c = c[c > 0]
+    for d in (3.0, 4.0, 5.0, 5.5, 5.8, 6.0, 6.2):
+        p = sum(_radius_sf_on_words(d / cj) for cj in c) / P.NOISE_PHASES
+        assert abs(p - norm.sf(d)) <= 2.0 ** -33, (d, p, norm.sf(d))
+        if d <= 5.5:
+            assert abs(p / norm.sf(d) - 1) < 1e-3, (d, p, norm.sf(d))
+
+
+def test_phase_words_are_their_own():
+    """Version 3 layout: the lane's outputs after the payload are (q0, w0, w1, w2, w3, q1, w4, ...);
+    noise sample n's phase is byte n & 3 of its q, low six bits."""
+    g = P.lane_generators(11, np.arange(3), 256)
+    h = P.lane_generators(11, np.arange(3), 256)
+    for n in range(9):
+        w, ph = g.noise_draw()
+        if n % 4 == 0:
+            q = h.next()
+        assert np.array_equal(w, h.next())
+        assert np.array_equal(ph, (q >> np.uint32(8 * (n % 4))) & np.uint32(63))
 
 
 def test_noise_is_complex_gaussian():
-    S, N, sigma = 400, 1024, 0.3
+    S, N, sigma = 1000, 1024, 0.3
     g = P.lane_generators(5, np.arange(S), N)
     n = P.lane_noise(g, S, N, sigma).ravel()
     for comp in (n.real, n.imag, (n * np.exp(-0.4j)).real):
@@ -106,9 +167,12 @@ def test_noise_is_complex_gaussian():
         assert abs(comp.var() / sigma ** 2 - 1) < 0.01
         k = np.mean((comp / sigma) ** 4)
         assert abs(k - 3) < 0.05
-        # tails: P(|n| > 3 sigma) = 2.7e-3, P(|n| > 4 sigma) = 6.3e-5
-        assert abs(np.mean(np.abs(comp) > 3 * sigma) / 2.6998e-3 - 1) < 0.05
-        assert abs(np.mean(np.abs(comp) > 4 * sigma) / 6.334e-5 - 1) < 0.25
+        # tails P(|n| > d sigma) within 4.5 binomial standard errors (z-scores printed)
+        for d in (1.0, 2.0, 3.0, 4.0):
+            q = 2 * norm.sf(d)
+            z = (np.mean(np.abs(comp) > d * sigma) - q) / np.sqrt(q * (1 - q) / comp.size)
+            print(f"d {d}: z {z:+.2f}")
+            assert abs(z) < 4.5, (d, z)
     assert abs(np.corrcoef(n.real, n.imag)[0, 1]) < 0.01
     # neighbouring time samples are uncorrelated
     assert abs(np.corrcoef(n.real[:-1], n.real[1:])[0, 1]) < 0.01
@@ -142,8 +206,9 @@ def test_noise_from_given_radii():
     bound is the product rounding alone; the float64 radius stays within its own bound of it."""
     w = np.random.default_rng(3).integers(0, 2 ** 32, size=20000, dtype=np.uint64).astype(np.uint32)
     sig = 0.21
-    n64, b64 = P.noise_from_words(w, sig, with_bound=True)
-    rad = lambda ws: np.sqrt(32.0 - np.log2((ws | P.NOISE_MASK).astype(np.float32).astype(np.float64))).astype(np.float32)
-    n32, b32 = P.noise_from_words(w, sig, with_bound=True, radius_fn=rad, product_rel=2.0 ** -53)
+    ph = np.random.default_rng(4).integers(0, P.NOISE_PHASES, size=w.size)
+    n64, b64 = P.noise_from_words(w, ph, sig, with_bound=True)
+    rad = lambda ws: np.sqrt(32.0 - np.log2((ws | P.RADIUS_OR).astype(np.float32).astype(np.float64))).astype(np.float32)
+    n32, b32 = P.noise_from_words(w, ph, sig, with_bound=True, radius_fn=rad, product_rel=2.0 ** -53)
     assert np.all(np.abs(n32 - n64) <= b64)
     assert np.all(b32 <= 2.0 ** -52 * np.abs(n32) + 1e-300)

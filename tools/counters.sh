@@ -9,7 +9,9 @@ mkdir -p $out
 args="--steps 2 --warmup 1 --no-cpu-baseline --no-ber-check --no-variant --ramp-seconds 0 $*"
 timeout -k 10 60 rocprofv3 -L > $out/avail.txt 2>&1 || true
 i=0
-IFS=';' read -ra GROUPS_ <<< "${COUNTER_GROUPS:-SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES;SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES;SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE}"
+# every pass also counts GRBM_GUI_ACTIVE (its own block): the kernel's duration in the same pass, from
+# which tools/pmc_summary.py --counters turns the SQ issue cycles into fractions of the SIMDs' time
+IFS=';' read -ra GROUPS_ <<< "${COUNTER_GROUPS:-SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE;SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 GRBM_GUI_ACTIVE}"
 for grp in "${GROUPS_[@]}"; do
     i=$((i+1))
     timeout -k 10 240 rocprofv3 --pmc $grp -d $out/g$i -o g$i --output-format csv -- python3 bench.py $args \
