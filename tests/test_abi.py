@@ -90,3 +90,30 @@ def test_product_library_has_no_ablation_switches():
     with open(B.lib_path(), "rb") as f:
         blob = f.read()
     assert b"OFDM_ABLATE" not in blob
+
+
+def test_ab_only_variant_reports_kernels_it_lacks():
+    """OFDM_AB_ONLY experiment builds (tools/ab.sh variants) instantiate N = 1024..4096 only.  Every
+    log2 N dispatch switch falls through to kOutOfRange, which such a build defines as kNotInBuild,
+    and the ABI turns that into OFDM_E_INVALID "kernel not in this build" (ValueError in Python)
+    instead of a HIP "invalid argument"; a product build keeps hipErrorInvalidValue there (N is
+    checked at plan creation, so it is never reached).  Checked on the sources, with the
+    preprocessor branches evaluated both ways."""
+    csrc = os.path.join(ROOT, "ofdm-based-systems_amd", "csrc")
+    inst = open(os.path.join(csrc, "ofdm_kernels_inst.hpp")).read()
+    launch = open(os.path.join(csrc, "ofdm_launch.hpp")).read()
+    abi = open(os.path.join(csrc, "ofdm_abi.hip")).read()
+    switches = re.findall(r"switch \(logn\) \{.*?default:\s*return (\w+);", inst, flags=re.S)
+    assert len(switches) == 3 and set(switches) == {"kOutOfRange"}, switches
+
+    def branch(text, name, ab_only):
+        m = re.search(r"#ifdef OFDM_AB_ONLY\n(.*?)#else\n(.*?)#endif", text[text.index(name) - 200:], flags=re.S)
+        return m.group(1 if ab_only else 2)
+
+    assert "kOutOfRange = kNotInBuild" in branch(inst, "constexpr hipError_t kOutOfRange", True)
+    assert "kOutOfRange = hipErrorInvalidValue" in branch(inst, "constexpr hipError_t kOutOfRange", False)
+    assert "kAbOnly = true" in branch(launch, "constexpr bool kAbOnly", True)
+    assert "kAbOnly = false" in branch(launch, "constexpr bool kAbOnly", False)
+    hipchk = abi[abi.index("#define HIPCHK"):abi.index("} while (0)", abi.index("#define HIPCHK"))]
+    assert "kAbOnly && _e == kNotInBuild" in hipchk and "OFDM_E_INVALID" in hipchk
+    assert "kernel not in this build" in hipchk
