@@ -152,6 +152,21 @@ def _cpu_worker(job, barrier, results):
     results.put((idx, S, t0, time.perf_counter()))
 
 
+def literal_reference(config: str):
+    """The literal reference's own CPU rate for this config (profiles/literal_reference_cpu.json:
+    its Simulation.run timed in the build container by the golden generators, tools/ref_cpu_rate.py),
+    reported beside the oracle port the box times; None when absent."""
+    path = os.path.join(ROOT, "profiles", "literal_reference_cpu.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f).get(config)
+    if not rec:
+        return None
+    return {"per_core_symbols_per_s": rec["per_core_symbols_per_s"], "cores": rec["cores"], "kind": "reference",
+            "measured": rec["measured"], "source": "profiles/literal_reference_cpu.json"}
+
+
 def cpu_baseline(cfg, per_worker: int):
     """The NumPy oracle (a port of the reference path, complex128 like the reference) on every
     CPU of this process's share, one worker process per core, bounded sample.  The workers start,
@@ -684,6 +699,9 @@ def main():
         # on rank 0 after every GPU measurement, for any number of ranks (the other ranks wait at
         # rt.finish()): the reference CPU path on the node's host cores, in the same run
         out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample or max(100, 30000 * 1024 // N))
+        lit = literal_reference(args.config)
+        if lit is not None:
+            out["cpu_baseline"]["literal_reference"] = lit
     if rt.rank == 0:
         print(json.dumps(out), flush=True)
     rt.finish()
