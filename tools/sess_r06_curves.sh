@@ -15,4 +15,11 @@ for cfg in d e; do
         2> gpurun_out/${TAG}_sweep_$cfg.err || { echo "sweep $cfg rc=$?"; tail -3 gpurun_out/${TAG}_sweep_$cfg.err; exit 1; }
     python -c "import json; d=json.load(open('gpurun_out/${TAG}_sweep_$cfg.json')); print('sweep $cfg', '%.4g'%d['value'], d['ms_per_step'])"
 done
+# the single point on one HIP stream lane (the bench default) against two and three (run k+1's TX
+# beside run k's RX), configs b and c, interleaved twice
+for rep in 1 2; do for cfg in b c; do for lanes in 1 2 3; do
+    timeout -k 10 180 python bench.py --config $cfg --lanes $lanes --steps 40 --warmup 5 --no-cpu-baseline --no-ber-check \
+        --no-variant > gpurun_out/${TAG}_lanes_${cfg}_${lanes}_$rep.json 2> gpurun_out/${TAG}_lanes.err || { echo "lanes rc=$?"; exit 1; }
+    python -c "import json; d=json.load(open('gpurun_out/${TAG}_lanes_${cfg}_${lanes}_$rep.json')); print('lanes', '$cfg', $lanes, $rep, '%.4g'%d['value'], round(d['ms_per_step'],3))"
+done; done; done
 exit 0
