@@ -221,7 +221,9 @@ class LinkEngine:
             # one collective on the TX -> RX critical path: every rank gathers all ranks'
             # ofdm_stats records and reduces them (combine_stats), so all ranks hold the
             # statistics -- and sigma -- of a single-GPU run, bit for bit
-            if world > 1:
+            # (run with any process group, one rank included: a 1-rank RCCL group exercises the
+            # same collectives, tests/test_gpu_multirank.py)
+            if group is not None:
                 import torch.distributed as dist
 
                 parts = [torch.empty_like(stats) for _ in range(world)]
@@ -249,7 +251,7 @@ class LinkEngine:
                 self.rx(stream, y, nr_d, ni_d, seed, stats, samples, snr_db, noise_on, bits_d, b0, nb,
                         n_valid, counters, z_out if zk else None, zk)
         work = None
-        if world > 1:
+        if group is not None:
             import torch.distributed as dist
 
             # off the critical path: the next run's TX does not wait for this reduction;
@@ -329,7 +331,7 @@ class LinkEngine:
                 y = torch.empty((max(mine, 1), self.ystride), dtype=self.cdtype, device=dev)
                 self._timed(events, "ofdm_tx", mine, lambda: self.tx(st, None, seed, lo, mine, y, stats))
                 work = None
-                if world > 1:
+                if group is not None:
                     import torch.distributed as dist
 
                     parts = [torch.empty_like(stats) for _ in range(world)]
@@ -349,7 +351,7 @@ class LinkEngine:
             self._timed(events, "ofdm_rx", mine, lambda: self.rx(
                 stream, y, None, None, seed, stats, samples, snr, True, None, lo, mine, n_valid, counters))
             red = None
-            if world > 1:
+            if group is not None:
                 import torch.distributed as dist
 
                 red = dist.all_reduce(counters, op=dist.ReduceOp.SUM, group=group, async_op=True)

@@ -1,7 +1,7 @@
 """Rank program of tests/test_gpu_multirank.py (not a test module): every rank binds device 0
-(OFDM_BENCH_DEVICE semantics -- RCCL refuses two ranks on one GPU, so the group is gloo), runs the
-complex128 throughput kernels of BASELINE configs (b) and (c) through LinkEngine's sharded schedules
-and rank 0 writes the per-run results as JSON."""
+(OFDM_BENCH_DEVICE semantics -- RCCL refuses two ranks on one GPU, so two ranks use gloo; one rank
+may use RCCL, argv[3] = "nccl"), runs the complex128 throughput kernels of BASELINE configs (b) and
+(c) through LinkEngine's sharded schedules and rank 0 writes the per-run results as JSON."""
 
 import json
 import os
@@ -22,8 +22,13 @@ def record(st):
 
 def main():
     out_path, S = sys.argv[1], int(sys.argv[2])
-    torch.cuda.set_device(int(os.environ.get("OFDM_BENCH_DEVICE", "0")))
-    dist.init_process_group("gloo")
+    backend = sys.argv[3] if len(sys.argv) > 3 else "gloo"
+    dev = int(os.environ.get("OFDM_BENCH_DEVICE", "0"))
+    torch.cuda.set_device(dev)
+    if backend == "nccl":  # as bench.py's Runtime binds it
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group(backend)
     g = dist.group.WORLD
     res = {}
     for cfg in ("b", "c"):
@@ -36,7 +41,7 @@ def main():
         res[cfg] = {"whole": record(whole), "batched": record(batched), "pipelined": [record(p) for p in piped]}
     if dist.get_rank() == 0:
         with open(out_path, "w") as f:
-            json.dump({"world": dist.get_world_size(), "runs": res}, f)
+            json.dump({"world": dist.get_world_size(), "backend": dist.get_backend(), "runs": res}, f)
     dist.barrier()
     dist.destroy_process_group()
 

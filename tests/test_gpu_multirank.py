@@ -36,8 +36,8 @@ def _env():
     return env
 
 
-def _launch(args, timeout):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+def _launch(args, timeout, nproc=2):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={_port()}"] + args
     return subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=timeout)
 
@@ -102,3 +102,25 @@ def test_bench_sweep_two_ranks_on_one_gpu(gpu, config):
     assert d2["sweep"]["snr_db"] == d1["sweep"]["snr_db"]
     assert d2["sweep"]["ber"] == d1["sweep"]["ber"], (d2["sweep"]["ber"], d1["sweep"]["ber"])
     assert d2["roofline"] is not None and d2["value"] > 0
+
+
+def test_rccl_group_of_one_rank_matches_no_group(gpu, tmp_path):
+    """The RCCL branch of the multi-GPU path on the one GPU a box has: one rank in an "nccl" (RCCL)
+    process group bound with device_id, as bench.py binds every rank of a node.  LinkEngine runs its
+    collectives for any group (engine.py: the device all-gather of the ofdm_stats records, the exact
+    limb reduction, the asynchronous counter all-reduce -- in run_async and in the pipelined
+    schedule), so this executes RCCL on the device tensors the 8-GPU run exchanges; the counts and
+    the power bits must equal the group-less run's."""
+    out = tmp_path / "rccl.json"
+    r = _launch([os.path.join(ROOT, "tests", "multirank_worker.py"), str(out), str(S), "nccl"], timeout=600, nproc=1)
+    assert r.returncode == 0, r.stderr[-4000:]
+    got = json.loads(out.read_text())
+    assert got["world"] == 1 and got["backend"] == "nccl"
+    for cfg in ("b", "c"):
+        c = bench.CONFIGS[cfg]
+        eng = bench.make_engine(c, "f64")
+        one = _record(eng.run(S, c[5], seed=3))
+        piped = [_record(eng.run(S, c[5], seed=sd)) for sd in (4, 5)]
+        runs = got["runs"][cfg]
+        assert runs["whole"] == one and runs["batched"] == one, (cfg, runs, one)
+        assert runs["pipelined"] == piped, (cfg, runs["pipelined"], piped)
