@@ -183,7 +183,9 @@ def cpu_baseline(cfg, per_worker: int):
         per_worker = 8 * math.ceil(per_worker / 8)
         chunk = 8 * math.ceil(chunk / 8)
     aff, quota = host_cpus()
-    workers = host_cores()
+    # (at most 32 workers: each spawned worker re-imports this module, torch included, ~0.4 GB; on a
+    # whole 8-GPU node the cgroup share can be 8x a 1-GPU box's 16 CPUs)
+    workers = min(host_cores(), 32)
     ctx = mp.get_context("spawn")
     barrier, results = ctx.Barrier(workers + 1), ctx.Queue()
     w0 = time.perf_counter()
@@ -202,7 +204,7 @@ def cpu_baseline(cfg, per_worker: int):
     return {
         "value": syms / slowest, "unit": "OFDM symbols/s", "cores": workers, "kind": "port",
         "affinity_cpus": aff, "cgroup_quota_cpus": quota, "host_cpu_count": os.cpu_count(),
-        "sample": f"{workers} worker processes (min(affinity set {aff}, cgroup quota {quota}) CPUs; the machine "
+        "sample": f"{workers} worker processes (min(affinity set {aff}, cgroup quota {quota}, 32) CPUs; the machine "
                   f"reports {os.cpu_count()}) x {per_worker} OFDM symbols of the same config through the NumPy "
                   f"oracle in complex128, in runs of {chunk} symbols with the reference's PCG64 bits + legacy-normal "
                   f"noise generated inside the timing; clock started per worker after a shared barrier (start-up "
