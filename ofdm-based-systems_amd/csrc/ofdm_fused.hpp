@@ -414,11 +414,35 @@ __device__ __forceinline__ u4 ref_lane(const TxRxCommon& a, int64_t s, int t) {
     return u4{w[0], w[1], w[2], w[3]};
 }
 
+// The same for adaptive loading (FB = 1): byte i = the b_k bits of subcarrier k = t + i TPS, read MSB
+// first at bit s bps + bitoff_k (constellation/adaptive.py:178-199: each OFDM symbol's bits laid out
+// subcarrier-major with variable b_k), zero for an unused subcarrier -- the lane byte the adaptive
+// kernels mask with (1 << b_k) - 1.  b_k <= 8 (the plan's upat: orders <= 256), so three bytes cover
+// any alignment.
+template <int TPS>
+__device__ __forceinline__ u4 ref_lane_adaptive(const TxRxCommon& a, int64_t s, int t) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    const int64_t bit0 = s * a.bps;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const ScInfo sc = a.sc[t + i * TPS];
+        if (sc.lut < 0 || sc.bits <= 0) continue;
+        const int64_t o = bit0 + sc.bitoff;
+        const int64_t B = o >> 3;
+        uint32_t v = 0;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) v = (v << 8) | (B + j < a.n_bytes ? (uint32_t)a.bits[B + j] : 0u);
+        v = (v >> (24 - (int)(o & 7) - sc.bits)) & ((1u << sc.bits) - 1u);
+        w[i >> 2] |= v << (8 * (i & 3));
+    }
+    return u4{w[0], w[1], w[2], w[3]};
+}
+
 // Per-element tx constellation indices of one symbol for this lane, from whichever
 // source the launch uses: the lane generator's first 128 bits (philox mode) or the
 // staged words (reference mode).  FB > 0: fixed b = FB, compile-time offsets.  In philox
-// mode the generator g continues into the lane's noise (RX).  REF (FB > 1): the throughput
-// kernel's lane block filled from the caller's bits instead (ref_lane).
+// mode the generator g continues into the lane's noise (RX).  REF: the throughput kernel's lane
+// block filled from the caller's bits instead (ref_lane; adaptive: ref_lane_adaptive).
 template <int FB, int TPS, bool REF = false>
 struct TxBits {
     u4 lane;
@@ -441,7 +465,9 @@ struct TxBits {
         W = Wslot;
         base_bit = 0;
         lane.x = lane.y = lane.z = lane.w = 0u;
-        if constexpr (REF && FB > 1) {
+        if constexpr (REF && FB == 1) {
+            if (active) lane = ref_lane_adaptive<TPS>(a, s, t);
+        } else if constexpr (REF && FB > 1) {
             if (active) lane = ref_lane<FB, TPS>(a, s, t);
         } else if (from_words) {
             if (active) base_bit = stage_words<TPS>(a, s, Wslot, t);

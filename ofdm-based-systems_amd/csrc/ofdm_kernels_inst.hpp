@@ -247,15 +247,18 @@ static hipError_t tx_fast(const TxArgs& a, int* grid, hipStream_t s) {
 // throughput kernels' REF instantiations -- the timed kernels' bodies with the bit and noise source
 // swapped (ref_lane, array normals) -- so the reference's own streams pin the benched FFT / FIR /
 // slicer / count code (tests/test_gpu_ref_streams.py): complex128, OFDM with a cyclic prefix, fixed
-// 64-QAM at N = 1024 (configs b, c) and 256-QAM at N = 4096 (config e), flat or <= 8-tap channels
-// within the window FIR's reach.  Everything else with caller bits takes the generic kernel.
+// 64-QAM at N = 1024 (configs b, c) and 256-QAM at N = 4096 (config e), adaptive square-QAM loading
+// at N = 2048 (config d, FB = 1), flat or <= 8-tap channels within the window FIR's reach.
+// Everything else with caller bits takes the generic kernel.
 template <typename R, int LOGN>
-constexpr int ref_fb() { return sizeof(R) == 8 ? (LOGN == 10 ? 6 : LOGN == 12 ? 8 : 0) : 0; }
+constexpr int ref_fb() { return sizeof(R) == 8 ? (LOGN == 10 ? 6 : LOGN == 11 ? 1 : LOGN == 12 ? 8 : 0) : 0; }
 
 template <typename R, int LOGN>
 static bool ref_shape(const TxRxCommon& c) {
-    return ref_fb<R, LOGN>() > 0 && c.bits != nullptr && !c.adaptive && !c.nn && c.psk_m == 0 && !c.scm && !c.zpad &&
-           c.b == ref_fb<R, LOGN>();
+    constexpr int FB = ref_fb<R, LOGN>();
+    if (FB == 0 || c.bits == nullptr || c.nn || c.scm || c.zpad) return false;
+    if (FB == 1) return c.adaptive && c.upat;  // (upat: square QAM of orders <= 256, the adaptive kernels')
+    return !c.adaptive && c.psk_m == 0 && c.b == FB;
 }
 
 template <typename R, int LOGN>
@@ -368,8 +371,10 @@ static hipError_t rx_one(const RxArgs& a, int* grid, hipStream_t s) {
     if constexpr (ref_fb<R, LOGN>() > 0) {
         // reference streams on a bench shape (see ref_shape): the REF receiver needs the caller's
         // normals and no received-symbol tap
+        // (MV: as the timed kernels -- compiled out of the fixed-QAM ones, and in the adaptive
+        // kernel's instantiation, where FB = 1 forces SC-OFDM and zero padding off)
         if (ref_shape<R, LOGN>(a.c) && a.nr != nullptr && a.z_out == nullptr)
-            return rx_eq<R, LOGN, ref_fb<R, LOGN>(), false, true>(a, grid, s);
+            return rx_eq<R, LOGN, ref_fb<R, LOGN>(), ref_fb<R, LOGN>() == 1, true>(a, grid, s);
     }
     if constexpr (sizeof(R) == 8 && LOGN >= kFastMinLogN) {
         if (a.c.adaptive && a.c.upat && a.c.bits == nullptr && a.nr == nullptr && a.z_out == nullptr &&
