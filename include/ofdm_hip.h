@@ -207,7 +207,8 @@ int ofdm_power(ofdm_plan_t plan, void* stream, const void* y, int64_t len, doubl
  * counter-based lane streams keyed by (seed, global symbol) (stream version 3 since ABI 5:
  * Philox4x32-10 seeding MWC64X; definition in csrc/ofdm_device.hpp, restated in
  * oracle/philox_streams.py).  Caller bits on the bench shapes (complex128 OFDM, cyclic prefix,
- * 64-QAM at N = 1024 or 256-QAM at N = 4096) run the throughput kernels with the bit -- and in
+ * 64-QAM at N = 1024, adaptive square-QAM loading at N = 2048 or 256-QAM at N = 4096) run the
+ * throughput kernels with the bit -- and in
  * ofdm_rx, with nr/ni and no z_out, the noise -- source swapped; other shapes the generic kernel.  n_sym = 0 is an empty call (returns 0, launches nothing).
  *
  * ofdm_tx: for global OFDM symbols [sym0, sym0+n_sym): map -> IFFT(ortho) (OFDM) or

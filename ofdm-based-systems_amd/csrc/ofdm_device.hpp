@@ -55,6 +55,18 @@ __device__ __forceinline__ cpx<R> rot90(cpx<R> a) {
 }
 template <typename R>
 __device__ __forceinline__ R norm2(cpx<R> a) { return a.re * a.re + a.im * a.im; }
+// max of two arithmetic results (the PAPR peak): v_max_* directly.  fmax() in IEEE mode quiets an
+// operand the compiler cannot prove canonical first -- a second v_max_f64 x, x per element of the
+// complex128 flat transmitter's peak scan.  Same result for every non-signalling input.
+template <typename R>
+__device__ __forceinline__ R peak_max(R a, R b) {
+    R r;
+    if constexpr (sizeof(R) == 8)
+        asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    else
+        asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // complex64 on the packed-f32 VALU: v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 do both
 // components in one issue slot (the f32 vector peak of CDNA4 is only reached packed);

@@ -778,7 +778,10 @@ __global__ __launch_bounds__((tx_block<R, FB, LOGN, LT, ZPW>()), (tx_waves<R, FB
                 for (int i = 0; i < E; ++i) {
                     const R p2 = norm2(x[i]);
                     pxs += p2;
-                    mxs = fmax(mxs, p2);
+                    // (complex128 flat channel: v_max_f64 directly, 15 VALU per symbol and lane fewer;
+                    // the window-FIR kernels schedule fmax without the quieting step already, and the
+                    // complex64 ones grow with it)
+                    mxs = (sizeof(R) == 8 && LT == 0) ? peak_max(mxs, p2) : fmax(mxs, p2);
                 }
                 pxs += prefix_sum([&](int i) { return norm2(x[i]); });
                 px += pxs;
