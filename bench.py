@@ -318,9 +318,13 @@ class Runtime:
         # OFDM_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal on a 1-GPU box
         # (with --backend gloo; RCCL refuses two ranks on one GPU)
         self.dev = int(os.environ.get("OFDM_BENCH_DEVICE", self.local))
+        self.backend = None
         if not cpu:
             torch.cuda.set_device(self.dev)
-        if self.world > 1:
+        # launched by torch.distributed.run (WORLD_SIZE set): the process group even for one rank, so
+        # that a one-GPU rehearsal runs every collective and barrier of a node's N-rank run -- RCCL
+        # bound with device_id plus the gloo host group (tests/test_gpu_multirank.py)
+        if "WORLD_SIZE" in os.environ:
             import torch.distributed as dist
 
             if backend == "nccl" and not cpu:
@@ -329,6 +333,7 @@ class Runtime:
                 dist.init_process_group(backend)
             self.group = dist.group.WORLD
             self.world = dist.get_world_size()
+            self.backend = dist.get_backend()
             # host-side group for the closing barrier: while rank 0 times the CPU baseline, the other
             # ranks wait on a socket (gloo) instead of a device collective whose host thread spins
             self.host_group = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else self.group
@@ -338,13 +343,13 @@ class Runtime:
             torch.cuda.synchronize()
 
     def barrier(self):
-        if self.world > 1:
+        if self.group is not None:
             import torch.distributed as dist
 
             dist.barrier()
 
     def max_over_ranks(self, x: float) -> float:
-        if self.world == 1:
+        if self.group is None:
             return x
         import torch.distributed as dist
 
@@ -353,7 +358,7 @@ class Runtime:
         return float(t.item())
 
     def gather(self, obj):
-        if self.world == 1:
+        if self.group is None:
             return [obj]
         import torch.distributed as dist
 
@@ -362,7 +367,7 @@ class Runtime:
         return out
 
     def finish(self):
-        if self.world > 1:
+        if self.group is not None:
             import torch.distributed as dist
 
             dist.barrier(group=self.host_group)
@@ -463,7 +468,7 @@ def measure(rt: Runtime, args, cfg, precision: str, per_gpu: int, factory, ramp:
         while True:
             done = torch.tensor([time.perf_counter() - t_ramp >= args.ramp_seconds], dtype=torch.int32,
                                 device="cpu" if rt.cpu else "cuda")
-            if rt.world > 1:
+            if rt.group is not None:
                 import torch.distributed as dist
 
                 dist.all_reduce(done, op=dist.ReduceOp.MIN)  # every rank runs the same number of steps
@@ -666,6 +671,7 @@ def main():
         "unit": "OFDM symbols/s",
         "n_gpus": rt.world,
         "devices": devices,
+        "process_group": rt.backend,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": head["ms_per_step"],
@@ -731,7 +737,7 @@ def sweep_main(rt: Runtime, args, cfg, factory):
         what = f"{desc.split(',')[0]} as the BASELINE configs[2] SNR sweep: 0..30 dB by 1 dB, 26..29 dB by 0.25 dB"
     out = {
         "metric": "OFDM symbols/sec (1/2/4/8 GPU) at N_FFT=1024 64-QAM; BER ΔdB vs ref",
-        "value": head["value"], "unit": "OFDM symbols/s", "n_gpus": rt.world, "devices": devices,
+        "value": head["value"], "unit": "OFDM symbols/s", "n_gpus": rt.world, "devices": devices, "process_group": rt.backend,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": head["dtype"],
         "data": "synthetic: Philox4x32-10 / MWC64X bits and Box-Muller AWGN generated on the GPU per (seed, symbol)",

@@ -80,6 +80,27 @@ def test_bench_two_ranks_on_one_gpu(gpu):
     assert d["dtype"].startswith("c128") and 1e-5 < d["ber"] < 1e-3
 
 
+def test_bench_one_rank_rccl_runs_the_node_path(gpu):
+    """bench.py under torch.distributed.run with one rank: the Runtime a node's N-GPU run builds --
+    an RCCL process group bound with device_id, the gloo host group, the barriers and the
+    max-over-ranks timing on RCCL, the device gather, the CPU baseline on rank 0 while the host
+    group waits -- on the one GPU a box has.  The line reports its process group and the same BER as
+    the plain one-process run over the same symbols."""
+    common = ["--gpus", "1", "--symbols", "100000", "--steps", "2", "--warmup", "1", "--no-ber-check",
+              "--no-variant", "--ramp-seconds", "0", "--cpu-sample", "100"]
+    r = _launch([os.path.join(ROOT, "bench.py"), "--backend", "nccl"] + common, timeout=600, nproc=1)
+    assert r.returncode == 0, r.stderr[-4000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert d["process_group"] == "nccl" and d["n_gpus"] == 1 and d["devices"] == [0], d
+    assert d["value"] > 0 and d["cpu_baseline"]["value"] > 0
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + common, env=_env(), capture_output=True,
+                        text=True, timeout=600)
+    assert r1.returncode == 0, r1.stderr[-4000:]
+    d1 = json.loads([x for x in r1.stdout.splitlines() if x.startswith("{")][0])
+    assert d1["process_group"] is None
+    assert d["ber"] == d1["ber"] and d["config"]["symbols_per_step"] == d1["config"]["symbols_per_step"]
+
+
 @pytest.mark.parametrize("config", ["c", "d", "e"])
 def test_bench_sweep_two_ranks_on_one_gpu(gpu, config):
     """bench.py --gpus 2 --sweep on device 0 (gloo; the rehearsal of the driver's multi-GPU sweep
