@@ -537,7 +537,10 @@ def measure_sweep(rt: Runtime, args, groups, precision: str, per_gpu: int, facto
     before any result is read) and symbol-sharded across ranks; W untimed steps, K timed."""
     engines = [factory(g, precision) for g, _ in groups]
     total = per_gpu * rt.world
-    lanes = args.lanes or 2
+    # four lanes (HIP streams, one hardware queue each): the short launches of one point's TX overlap
+    # the others' RX and fill their start / drain bubbles -- config c's sweep 1.219-1.236e8 at two
+    # lanes against 1.243-1.251e8 at four, same box (profiles/r06p_sweep_lanes_c.txt)
+    lanes = args.lanes or 4
     for eng in engines:
         eng.reserve(total, 2, group=rt.group, lanes=lanes)
     npts = sum(len(q) for _, q in groups)
@@ -633,8 +636,9 @@ def main():
                          "adaptive; 10..30 dB by 5 at 16/64/256-QAM); --symbols per GPU per point (default 1e5 x 1024/N)")
     ap.add_argument("--lanes", type=int, default=None,
                     help="HIP streams the timed runs alternate over (LinkEngine.run_pipelined); default 1, "
-                         "--sweep 2 (its 1e5-symbol points overlap a receiver with the next transmitter: "
-                         "1.02 -> 1.08e8 symbols/s, profiles/r04c_sweep_c*.json)")
+                         "--sweep 4 (its 1e5-symbol points overlap receivers with the next transmitters: "
+                         "1.02 -> 1.08e8 symbols/s at 2, profiles/r04c_sweep_c*.json; 2 -> 4: +1.4 %, "
+                         "profiles/r06p_sweep_lanes_c.txt)")
     ap.add_argument("--ref-symbols", type=int, default=12000,
                     help="--sweep: reference-stream OFDM symbols per point near the BER 1e-4 crossing (26..29 dB)")
     args = ap.parse_args()
