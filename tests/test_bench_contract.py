@@ -75,6 +75,38 @@ def test_bench_gpus_flag_launches_ranks(gpus):
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["unit"] == "OFDM symbols/s"
 
 
+def test_bench_one_rank_under_torchrun_takes_the_process_group():
+    """A torch.distributed.run launch builds the process group even for one rank (bench.Runtime), so
+    one device rehearses the barriers, max-over-ranks timing and gather of a node's run; a plain
+    one-process run has none.  CPU engine double, gloo."""
+    import socket
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle"),
+                                         os.path.join(ROOT, "ofdm-based-systems_amd"), env.get("PYTHONPATH", "")])
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    args = [os.path.join(ROOT, "bench.py"), "--gpus", "1", "--backend", "gloo", "--engine-factory",
+            "bench_double:make_engine", "--config", "b", "--symbols", "3", "--steps", "2", "--warmup", "1",
+            "--cpu-sample", "2", "--no-ber-check", "--no-variant", "--ramp-seconds", "0"]
+    lines = {}
+    for name, cmd in (("torchrun", [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                                    "--master-addr=127.0.0.1", f"--master-port={port}"] + args),
+                      ("plain", [sys.executable] + args)):
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, (name, r.stderr[-3000:])
+        lines[name] = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert lines["torchrun"]["process_group"] == "gloo" and lines["plain"]["process_group"] is None
+    for d in lines.values():
+        assert d["n_gpus"] == 1 and d["devices"] == ["cpu"] and d["cpu_baseline"]["value"] > 0
+    assert lines["torchrun"]["ber"] == lines["plain"]["ber"]
+
+
 def test_sweep_grid_and_crossing():
     """--sweep: BASELINE configs[2]'s 0..30 dB in 1 dB steps plus SURVEY 8(d)'s 0.25 dB refinement
     over 26..29 dB; the crossing interpolates log10 BER linearly in dB."""
